@@ -1,0 +1,187 @@
+/*
+ * pss_hip.h -- C ABI of libpss_hip.so, the MI355X (gfx950) engine behind
+ * PsrSigSim's filterbank synthesis path.
+ *
+ * The reference has no FFI: its boundary is the Python method API (SURVEY.md
+ * §8(b)).  Each entry point below replaces one reference call (or a fused run
+ * of several), cited file:line against /root/reference/psrsigsim.  The Python
+ * layer (psrsigsim_amd, ctypes) mirrors the reference classes and calls these.
+ *
+ * Conventions
+ *  - All buffers are DEVICE pointers owned by the caller (torch); the library
+ *    never allocates or frees user memory.  Row-major [chan][sample] fp32.
+ *  - Every call is stream-ordered on `stream` (a hipStream_t; NULL = default)
+ *    and performs no host synchronisation; it is graph-capturable.
+ *  - Return codes: PSS_OK = 0, PSS_EINVAL = -1 (-> ValueError),
+ *    PSS_EUNSUPPORTED = -2 (-> NotImplementedError), PSS_EHIP = -3
+ *    (-> RuntimeError); pss_last_error() returns the message.
+ *  - Randomness is counter-based Philox4x32-10 keyed by (seed, call id,
+ *    purpose, GLOBAL channel, sample): results do not depend on how channels
+ *    are split across launches or GPUs.
+ */
+#ifndef PSS_HIP_H
+#define PSS_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSS_OK 0
+#define PSS_EINVAL (-1)
+#define PSS_EUNSUPPORTED (-2)
+#define PSS_EHIP (-3)
+
+/* source of the real (data) part */
+#define PSS_SRC_LOAD 0   /* read `data` (an already materialised signal)       */
+#define PSS_SRC_SEARCH 1 /* pulsar.py:222-244 PCHIP(phase) x chi2(df) x norm    */
+#define PSS_SRC_FOLD 2   /* pulsar.py:196-221 tile(profile) x chi2(Nfold) x norm */
+
+/* null stage */
+#define PSS_NULL_NONE 0
+#define PSS_NULL_UNDELAYED 1 /* pulsar.py:292-304: replace boxes, shared vector  */
+#define PSS_NULL_DELAYED 2   /* pulsar.py:306-330: chi2(100) box mask shifted
+                                through the same FFT, thresholded > 1           */
+
+/* observe() copy ("out") dtypes */
+#define PSS_OUT_NONE 0
+#define PSS_OUT_F32 1
+#define PSS_OUT_I8 2
+
+/*
+ * One fused run of the synthesis path over `nchan` rows:
+ *
+ *   source  ->  [delay ramp: rfft -> exp(-2 pi i f tau) -> irfft]  ->  [null]
+ *           ->  [radiometer noise]  ->  data      (+ optional pre-noise `out`)
+ *
+ * Replaces, for one signal, the sequence
+ *   Pulsar.make_pulses        pulsar/pulsar.py:107-151,185-244
+ *   ISM.disperse / FD_shift / scatter_broaden(convolve=False)
+ *                             ism/ism.py:20-74, 100-156, 158-220
+ *                             (each = per-channel utils.shift_t, utils/utils.py:17-59)
+ *   Pulsar.null               pulsar/pulsar.py:246-333
+ *   Telescope.observe (copy branch) + Receiver.radiometer_noise
+ *                             telescope/telescope.py:72-149, receiver.py:82-172
+ * with any prefix/subset of the stages enabled.  Several delay stages are
+ * fused into one forward/inverse FFT pair: phase exp(-2 pi i k sum(s_j)/N) on
+ * every bin, and on the Nyquist bin the product of the per-stage factors
+ * cos(pi s_j) that the reference's irfft imposes.
+ */
+typedef struct PssPipeline {
+    /* geometry */
+    int32_t nchan;      /* rows in this launch                                  */
+    int32_t chan0;      /* global channel index of row 0 (RNG key, table rows)  */
+    int64_t nsamp;      /* N: samples per row (= data.shape[1])                */
+    int64_t ld;         /* row stride of `data` in elements                     */
+    float *data;        /* [nchan][ld] in/out                                   */
+    void *work;         /* workspace, >= pss_workspace_bytes(nchan, nsamp)      */
+
+    /* source */
+    int32_t src;        /* PSS_SRC_*                                            */
+    int32_t prof_rows;  /* rows of `prof` (1 = same profile for every channel)  */
+    const float *prof;  /* SEARCH: [prof_rows][nint][4] PCHIP coefficients in the
+                           local interval coordinate u in [0,1): c3 u^3+c2 u^2+c1 u+c0
+                           FOLD: [prof_rows][nph] profile samples              */
+    int32_t nint;       /* SEARCH: number of PCHIP intervals                    */
+    int32_t nph;        /* FOLD: phase bins per period; NULL: box length        */
+    uint64_t phase_step;/* SEARCH: 2^64 / (samples per period), i.e. the pulse
+                           phase advance per sample in 2^-64 cycles             */
+    uint32_t knot_m;    /* SEARCH: 1/knot spacing (intervals per cycle)         */
+    float gen_df;       /* chi2 degrees of freedom of the pulse draws           */
+    float draw_norm;    /* signal._draw_norm                                    */
+
+    /* delay ramp (fused delay stages) -- all arrays indexed by local row       */
+    int32_t shift;          /* 1: run the FFT delay engine                     */
+    int32_t data_in_fft;    /* 1: real part carries the data through the FFT;
+                               0: the epilogue reads `data` unshifted (only the
+                               null mask goes through the FFT)                  */
+    const uint64_t *ramp;   /* [nchan] frac(s/N) in 2^-64 cycles, s = total delay
+                               in samples: bin k gets exp(-2 pi i k' s / N)     */
+    const float *nyq_re;    /* [nchan] Nyquist factor for the real part         */
+    const float *nyq_im;    /* [nchan] Nyquist factor for the imaginary part    */
+
+    /* null */
+    int32_t null_mode;      /* PSS_NULL_*                                       */
+    int32_t null_slots;     /* length of null_rank (= nsub)                     */
+    const int32_t *null_rank;  /* [null_slots] order of the nulled pulse in the
+                               reference's np.random.choice list, or -1         */
+    int64_t null_shift;     /* shift_val (pulsar.py:286)                        */
+    float null_box_df;      /* chi2 df of the box values (mask / undelayed)     */
+    float null_box_scale;   /* box scale: draw_norm (mask) or draw_norm*opm     */
+    float null_rep_df;      /* DELAYED: df of the replacement draws             */
+    float null_rep_scale;   /* DELAYED: draw_norm * off-pulse mean              */
+
+    /* radiometer noise */
+    int32_t noise;          /* 1: data += noise_norm * chi2(noise_df)           */
+    float noise_df;
+    float noise_norm;
+
+    /* observe() pre-noise copy */
+    int32_t out_kind;       /* PSS_OUT_*                                        */
+    void *out;              /* [nchan][nsamp] float32 or int8                   */
+    float clip;             /* out = min(pre-noise, clip) (telescope.py:140-145)*/
+
+    /* randomness */
+    uint64_t seed;
+    uint32_t call_gen;      /* call ids: one per API call that drew randomness  */
+    uint32_t call_null;     /* (make_pulses / null / noise), so that repeated   */
+    uint32_t call_noise;    /* calls draw fresh values, like np.random          */
+
+    /* exact mode: injected draws (NULL = use Philox) */
+    const float *inj_gen;     /* [nchan][nsamp] pulse chi2 draws                */
+    const float *inj_box;     /* [nsamp] box values (already scaled), shared    */
+    const float *inj_rep;     /* [nchan][nsamp] DELAYED replacement values      */
+    const float *inj_noise;   /* [nchan][nsamp] noise chi2 draws                */
+} PssPipeline;
+
+/* Library / device info. */
+int pss_version(void);
+int pss_last_error(char *buf, size_t n);
+
+/* Workspace bytes the fused run needs for `nchan` rows of length `nsamp`. */
+int64_t pss_workspace_bytes(int32_t nchan, int64_t nsamp);
+
+/* The fused run (see PssPipeline). */
+int pss_run(const PssPipeline *p, void *stream);
+
+/*
+ * utils.shift_t on a batch of rows (utils/utils.py:17-59): every row r is
+ * shifted by shift_samples[r] (= shift/dt, may be fractional) through the same
+ * FFT engine.  Even N only (odd N: the reference's irfft returns N-1 samples
+ * and the row assignment raises -> PSS_EINVAL).  `nyq` is the Nyquist factor
+ * per row (cos(pi*s) for one reference call).  In place.
+ */
+int pss_shift_rows(float *rows, int32_t nrows, int64_t n, int64_t ld,
+                   const uint64_t *ramp, const float *nyq, void *work, void *stream);
+
+/* utils.down_sample per row (utils/utils.py:62-68): out[r][i] = mean of
+ * in[r][i*fact : (i+1)*fact]; in_len must be a multiple of fact. */
+int pss_down_sample(const float *in, float *out, int32_t nrows, int64_t in_len,
+                    int64_t in_ld, int32_t fact, void *stream);
+
+/* utils.rebin per row (utils/utils.py:71-91): `lo`/`hi` are the integer window
+ * edges [lo_i, hi_i) the reference derives from its ceil() arithmetic. */
+int pss_rebin(const float *in, float *out, int32_t nrows, int64_t in_len, int64_t in_ld,
+              int32_t newlen, const int64_t *lo, const int64_t *hi, void *stream);
+
+/* Telescope.observe tail (telescope.py:140-145): clip from above at `clip`,
+ * cast to float32 or int8 (truncation toward zero, as numpy's astype). */
+int pss_clip_cast(const float *in, void *out, int64_t count, float clip, int32_t out_kind,
+                  void *stream);
+
+/* Backend.fold (telescope/backend.py:34-49): out[c][b] =
+ * sum_{f<n_fold} data[c][npbins + f*half + b], half = npbins/2. */
+int pss_fold(const float *data, float *out, int32_t nchan, int64_t ld, int64_t npbins,
+             int64_t n_fold, void *stream);
+
+/* Philox chi2 draws (test hook + CPU-independent statistics checks):
+ * out[r][n] = chi2(df) keyed like the pipeline's purpose `purpose`. */
+int pss_chi2_fill(float *out, int32_t nrows, int32_t chan0, int64_t n, float df,
+                  uint64_t seed, uint32_t call_id, uint32_t purpose, void *stream);
+
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSS_HIP_H */

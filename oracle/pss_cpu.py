@@ -343,25 +343,32 @@ def null(sig, psr, null_frac, draws, length=None, frequency=None):
     pulses = draws.choice(sig.nsub, npulse)
     N = sig.data.shape[1]
     opm = np.mean(psr.Profiles._max_profile[opw.astype(int)])
+    box_row = np.zeros(N)          # test-side record of the (pre-shift) box values
+    rep_dense = None
     if sig.delay is None:
         for p in pulses:
             bins = np.arange(Nph * p, Nph * (p + 1)) + shift_val
             bins = bins[bins < N]
             noise = draws.chi2(df, len(bins)) * sig.draw_norm
             sig.data[:, bins] = noise * opm
+            box_row[bins] = noise * opm
     else:
         mask = np.zeros(sig.data.shape)
         for p in pulses:
             bins = np.arange(Nph * p, Nph * (p + 1)) + shift_val
             bins = bins[bins < N]
             mask[:, bins] = draws.chi2(check_df, len(bins)) * sig.draw_norm
+        box_row[:] = mask[0]
         dt_ms = (1.0 / sig.samprate) * 1e-3     # (1/samprate).to('ms')
         for c in range(sig.nchan):
             mask[c, :] = shift_t(mask[c, :], sig.delay[c], dt=dt_ms)
         hit = np.where(mask > 1)
         noise = draws.chi2(df, np.shape(hit)[1]) * sig.draw_norm
         sig.data[hit] = noise * opm
-    return {"shift_val": shift_val, "pulses": pulses, "opw": opw, "opm": opm}
+        rep_dense = np.zeros(sig.data.shape)
+        rep_dense[hit] = noise * opm
+    return {"shift_val": shift_val, "pulses": pulses, "opw": opw, "opm": opm,
+            "box_row": box_row, "rep_dense": rep_dense}
 
 
 # ---------------------------------------------------------------------------

@@ -1,0 +1,329 @@
+"""Deferred, fused execution of the synthesis path on the GPU.
+
+The reference mutates ``signal._data`` eagerly, one NumPy pass per call
+(make_pulses, each shift_t loop, null, noise).  Here every call records a
+*stage* on the signal's pending pipeline; the pipeline is executed -- as ONE
+fused run of the HIP engine (pss_run) -- when the data is needed
+(``signal.data``), when the next call cannot be appended (e.g. a delay after
+noise), or by Telescope.observe.  Stage order is the reference's:
+
+    source (make_pulses | existing data) -> delay stages* -> null -> noise
+
+Results are identical to running the stages one by one: several delay stages
+compose into a single ramp (phase = sum of delays, Nyquist factor = product of
+the per-stage cos(pi s)), and the delayed-null mask rides through the same FFT
+as the imaginary part of the transformed row.
+
+Randomness: counter-based Philox keyed by (seed, call id, purpose, GLOBAL
+channel, sample) -- see ``seed()``; exact replay of the reference's own draws
+is available through ``inject()`` (tests).
+"""
+import ctypes
+import threading
+
+import numpy as np
+import torch
+
+from . import _lib
+
+# ---------------------------------------------------------------------------
+# randomness
+# ---------------------------------------------------------------------------
+_state = {"seed": 0x5EED1776, "calls": 0}
+_lock = threading.Lock()
+
+
+def seed(s):
+    """Seed the engine's Philox streams (the analogue of ``np.random.seed``).
+    Resets the call counter so a seeded sequence of calls is reproducible."""
+    with _lock:
+        _state["seed"] = int(s) & 0xFFFFFFFFFFFFFFFF
+        _state["calls"] = 0
+
+
+def next_call():
+    with _lock:
+        _state["calls"] += 1
+        return _state["calls"] & 0x0FFFFFFF
+
+
+def host_rng(call_id):
+    """numpy Generator for small host-side draws (null pulse choice), keyed
+    like the device streams so every shard makes the same choice."""
+    return np.random.Generator(np.random.Philox(key=[_state["seed"], call_id]))
+
+
+# exact mode: draws to use instead of Philox, consumed by the next pipeline
+# stage of that kind (tests replay the reference's recorded draws).
+_inject = {}
+
+
+def inject(**kw):
+    """inject(gen=, box=, rep=, noise=, null_pulses=) -- host arrays (global
+    channel x sample, or one row for `box`) used by the next stage of that
+    kind instead of Philox draws."""
+    for k, v in kw.items():
+        if k not in ("gen", "box", "rep", "noise", "null_pulses"):
+            raise KeyError(k)
+        _inject[k] = v
+
+
+def take_injection(kind):
+    return _inject.pop(kind, None)
+
+
+def clear_injections():
+    _inject.clear()
+
+
+# ---------------------------------------------------------------------------
+# device helpers
+# ---------------------------------------------------------------------------
+def device():
+    _lib.lib()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_ptr():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+_ws = {}
+
+
+def workspace(nbytes):
+    """Cached per-device workspace (grown on demand, never shrunk)."""
+    dev = device()
+    buf = _ws.get(dev.index)
+    if nbytes <= 0:
+        return None
+    if buf is None or buf.numel() < nbytes:
+        _ws.pop(dev.index, None)
+        buf = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
+        _ws[dev.index] = buf
+    return buf
+
+
+def release_workspace():
+    _ws.clear()
+
+
+def to_dev(a, dtype=None):
+    t = torch.as_tensor(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.to(device())
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def ramp_words(samples, N):
+    """frac(s/N) * 2^64 as uint64 (bin k gets exp(-2 pi i k s / N))."""
+    x = np.asarray(samples, dtype=np.float64) / float(N)
+    f = x - np.floor(x)
+    w = np.ldexp(f, 64)
+    w = np.where(w >= 2.0 ** 64, 0.0, w)
+    hi = np.floor(w / 2.0 ** 32)
+    lo = w - hi * 2.0 ** 32
+    return (hi.astype(np.uint64) << np.uint64(32)) | lo.astype(np.uint64)
+
+
+def u64_to_i64_tensor(u):
+    return to_dev(np.asarray(u, dtype=np.uint64).view(np.int64))
+
+
+# ---------------------------------------------------------------------------
+# pending pipeline
+# ---------------------------------------------------------------------------
+class Source(object):
+    """make_pulses stage (pulsar.py:185-244).  mode 'search' evaluates the
+    PCHIP table at the pulse phase of every sample; 'fold' tiles an Nph-bin
+    profile table.  Tables are global over channels (prof_rows == Nchan) or
+    a single shared row."""
+
+    def __init__(self, mode, table, df, draw_norm, call_id, nph=0, M=0, nint=0,
+                 phase_step=0, inj=None):
+        self.mode = mode
+        self.table = table            # np.float32, search [rows,nint,4] / fold [rows,nph]
+        self.df = float(df)
+        self.draw_norm = float(draw_norm)
+        self.call_id = call_id
+        self.nph = int(nph)
+        self.M = int(M)
+        self.nint = int(nint)
+        self.phase_step = int(phase_step)
+        self.inj = inj                # global [Nchan, N] draws or None
+
+
+class Pending(object):
+    def __init__(self, source=None):
+        self.source = source          # None -> load existing data
+        self.shifts = []              # list of np.float64 [Nchan_global] (samples)
+        self.null = None              # dict
+        self.noise = None             # dict
+        self.out = None               # dict(kind, tensor, clip)
+
+    def empty(self):
+        return (self.source is None and not self.shifts and self.null is None
+                and self.noise is None and self.out is None)
+
+
+def build_pipeline(sig, pend, rows, chan0, data, out=None, global_rows=None):
+    """A PssPipeline for local rows [0, rows) whose global channels start at
+    ``chan0`` (or are listed in ``global_rows``).  Returns (struct, keepalive)."""
+    N = sig._ncols
+    p = _lib.PssPipeline()
+    keep = []
+    gidx = np.arange(chan0, chan0 + rows) if global_rows is None else np.asarray(global_rows)
+    p.nchan = rows
+    p.chan0 = int(gidx[0])
+    p.nsamp = N
+    p.ld = data.stride(0)
+    p.data = ptr(data)
+    p.seed = _state["seed"]
+    src = pend.source
+    if src is None:
+        p.src = _lib.SRC_LOAD
+    else:
+        p.src = _lib.SRC_SEARCH if src.mode == "search" else _lib.SRC_FOLD
+        # rows are indexed by GLOBAL channel inside the kernel (or row 0 when
+        # the table is shared); the device copy is cached on the stage.
+        if getattr(src, "dev_table", None) is None:
+            src.dev_table = to_dev(src.table)
+        tt = src.dev_table
+        p.prof_rows = src.table.shape[0]
+        p.prof = ptr(tt)
+        p.nint = src.nint
+        p.nph = src.nph
+        p.phase_step = src.phase_step
+        p.knot_m = src.M
+        p.gen_df = src.df
+        p.draw_norm = src.draw_norm
+        p.call_gen = src.call_id
+        if src.inj is not None:
+            t = to_dev(np.asarray(src.inj, dtype=np.float32)[gidx])
+            keep.append(t)
+            p.inj_gen = ptr(t)
+    need_fft = bool(pend.shifts) or (pend.null is not None and pend.null["mode"] == "delayed")
+    if need_fft:
+        if N % 2:
+            raise ValueError("could not broadcast input array from shape (%d,) into shape (%d,)"
+                             % (N - 1, N))
+        p.shift = 1
+        total = np.zeros(sig.Nchan)
+        nyq_re = np.ones(sig.Nchan)
+        for s in pend.shifts:
+            total = total + s
+            nyq_re = nyq_re * np.cos(np.pi * s)
+        nul = pend.null
+        if nul is not None and nul["mode"] == "delayed":
+            mask_total = nul["mask_samples"]
+            nyq_im = np.cos(np.pi * mask_total)
+            if pend.shifts:
+                p.data_in_fft = 1
+                ramp_s = total
+            else:
+                p.data_in_fft = 0
+                ramp_s = mask_total
+        else:
+            p.data_in_fft = 1
+            ramp_s = total
+            nyq_im = nyq_re
+        r = u64_to_i64_tensor(ramp_words(ramp_s[gidx], N))
+        a = to_dev(nyq_re[gidx].astype(np.float32))
+        b = to_dev(nyq_im[gidx].astype(np.float32))
+        keep += [r, a, b]
+        p.ramp, p.nyq_re, p.nyq_im = ptr(r), ptr(a), ptr(b)
+        wb = _lib.load().pss_workspace_bytes(rows, N)
+        ws = workspace(wb)
+        p.work = ptr(ws) if ws is not None else None
+    nul = pend.null
+    if nul is not None:
+        p.null_mode = _lib.NULL_DELAYED if nul["mode"] == "delayed" else _lib.NULL_UNDELAYED
+        rk = to_dev(nul["rank"].astype(np.int32))
+        keep.append(rk)
+        p.null_rank = ptr(rk)
+        p.null_slots = int(nul["rank"].size)
+        p.null_shift = int(nul["shift_val"])
+        p.nph = int(nul["nph"])
+        p.null_box_df = nul["box_df"]
+        p.null_box_scale = nul["box_scale"]
+        p.null_rep_df = nul.get("rep_df", 1.0)
+        p.null_rep_scale = nul.get("rep_scale", 0.0)
+        p.call_null = nul["call_id"]
+        if nul.get("inj_box") is not None:
+            t = to_dev(np.asarray(nul["inj_box"], dtype=np.float32))
+            keep.append(t)
+            p.inj_box = ptr(t)
+        if nul.get("inj_rep") is not None:
+            t = to_dev(np.asarray(nul["inj_rep"], dtype=np.float32)[gidx])
+            keep.append(t)
+            p.inj_rep = ptr(t)
+    noi = pend.noise
+    if noi is not None:
+        p.noise = 1
+        p.noise_df = noi["df"]
+        p.noise_norm = noi["norm"]
+        p.call_noise = noi["call_id"]
+        if noi.get("inj") is not None:
+            t = to_dev(np.asarray(noi["inj"], dtype=np.float32)[gidx])
+            keep.append(t)
+            p.inj_noise = ptr(t)
+    if out is not None:
+        p.out_kind = out["kind"]
+        p.out = ptr(out["tensor"])
+        p.clip = out["clip"]
+    return p, keep
+
+
+def run(p, keep):
+    rc = _lib.lib().pss_run(ctypes.byref(p), stream_ptr())
+    _lib.check(rc, "pss_run")
+    return keep
+
+
+def execute(sig, pend):
+    """Run ``pend`` over the signal's local rows (allocating the buffer when
+    the source generates it) and over the shadow of global channel 0."""
+    N = sig._ncols
+    rows = sig._c1 - sig._c0
+    if sig._buf is None or tuple(sig._buf.shape) != (rows, N):
+        if pend.source is None:
+            raise RuntimeError("signal has no data")
+        sig._buf = torch.empty((rows, N), dtype=torch.float32, device=device())
+    out = pend.out
+    if sig._c0 > 0 and sig._track_row0:
+        # shadow of global channel 0 (shard-invariant null()): same stages
+        if sig._row0 is None or sig._row0.shape[1] != N:
+            if pend.source is None:
+                raise RuntimeError("channel-0 shadow lost")
+            sig._row0 = torch.empty((1, N), dtype=torch.float32, device=device())
+        p0, k0 = build_pipeline(sig, pend, 1, 0, sig._row0)
+        run(p0, k0)
+    p, keep = build_pipeline(sig, pend, rows, sig._c0, sig._buf, out=out)
+    run(p, keep)
+
+
+def probe_row0(sig, pend, count):
+    """First ``count`` samples of GLOBAL channel 0 after ``pend`` (without
+    noise), on any shard: replayed from the source when it is generated,
+    else read from the local buffer or the channel-0 shadow."""
+    N = sig._ncols
+    base = None
+    if pend.source is None:
+        base = sig._buf[0:1] if sig._c0 == 0 else sig._row0
+        if base is None:
+            raise RuntimeError("no data for channel 0")
+    scratch = torch.empty((1, N), dtype=torch.float32, device=device())
+    if base is not None:
+        scratch.copy_(base)
+    probe = Pending(pend.source)
+    probe.shifts = list(pend.shifts)
+    probe.null = pend.null
+    if probe.empty():
+        return scratch[0, :count].cpu().numpy()
+    p, keep = build_pipeline(sig, probe, 1, 0, scratch)
+    run(p, keep)
+    return scratch[0, :count].cpu().numpy().astype(np.float64)

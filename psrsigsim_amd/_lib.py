@@ -1,0 +1,104 @@
+"""ctypes binding of libpss_hip.so (include/pss_hip.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU
+is visible, every compute call raises.  ``lib()`` loads the in-tree build
+(``psrsigsim_amd/libpss_hip.so``, produced by ``__graft_entry__.build()`` /
+``psrsigsim_amd/build.py``).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpss_hip.so")
+
+PSS_OK, PSS_EINVAL, PSS_EUNSUPPORTED, PSS_EHIP = 0, -1, -2, -3
+SRC_LOAD, SRC_SEARCH, SRC_FOLD = 0, 1, 2
+NULL_NONE, NULL_UNDELAYED, NULL_DELAYED = 0, 1, 2
+OUT_NONE, OUT_F32, OUT_I8 = 0, 1, 2
+P_PULSE, P_BOX, P_REP, P_NOISE, P_TEST = 1, 2, 3, 4, 5
+
+c_i32, c_i64, c_u32, c_u64, c_f32, c_vp = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
+                                           ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
+
+
+class PssPipeline(ctypes.Structure):
+    """Mirror of ``struct PssPipeline`` (include/pss_hip.h); field order and
+    types must match exactly (checked by tests/test_cabi.py)."""
+    _fields_ = [
+        ("nchan", c_i32), ("chan0", c_i32), ("nsamp", c_i64), ("ld", c_i64),
+        ("data", c_vp), ("work", c_vp),
+        ("src", c_i32), ("prof_rows", c_i32), ("prof", c_vp), ("nint", c_i32), ("nph", c_i32),
+        ("phase_step", c_u64), ("knot_m", c_u32), ("gen_df", c_f32), ("draw_norm", c_f32),
+        ("shift", c_i32), ("data_in_fft", c_i32), ("ramp", c_vp), ("nyq_re", c_vp), ("nyq_im", c_vp),
+        ("null_mode", c_i32), ("null_slots", c_i32), ("null_rank", c_vp), ("null_shift", c_i64),
+        ("null_box_df", c_f32), ("null_box_scale", c_f32), ("null_rep_df", c_f32),
+        ("null_rep_scale", c_f32),
+        ("noise", c_i32), ("noise_df", c_f32), ("noise_norm", c_f32),
+        ("out_kind", c_i32), ("out", c_vp), ("clip", c_f32),
+        ("seed", c_u64), ("call_gen", c_u32), ("call_null", c_u32), ("call_noise", c_u32),
+        ("inj_gen", c_vp), ("inj_box", c_vp), ("inj_rep", c_vp), ("inj_noise", c_vp),
+    ]
+
+
+EXPORTS = {
+    "pss_version": (ctypes.c_int, []),
+    "pss_last_error": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
+    "pss_workspace_bytes": (c_i64, [c_i32, c_i64]),
+    "pss_run": (ctypes.c_int, [ctypes.POINTER(PssPipeline), c_vp]),
+    "pss_shift_rows": (ctypes.c_int, [c_vp, c_i32, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "pss_down_sample": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_vp]),
+    "pss_rebin": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp]),
+    "pss_clip_cast": (ctypes.c_int, [c_vp, c_vp, c_i64, c_f32, c_i32, c_vp]),
+    "pss_fold": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp]),
+    "pss_chi2_fill": (ctypes.c_int, [c_vp, c_i32, c_i32, c_i64, c_f32, c_u64, c_u32, c_u32, c_vp]),
+}
+
+_LIB = None
+
+
+class HipUnavailable(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load the shared library and declare every export (no GPU needed)."""
+    global _LIB
+    if _LIB is not None and path == LIB_PATH:
+        return _LIB
+    if not os.path.exists(path):
+        raise HipUnavailable("libpss_hip.so not built at %s -- run `python -c 'import "
+                             "__graft_entry__ as g; g.build()'`" % path)
+    L = ctypes.CDLL(path)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path == LIB_PATH:
+        _LIB = L
+    return L
+
+
+def lib():
+    """The library, for compute: also requires a visible HIP device."""
+    L = load()
+    import torch
+    if not torch.cuda.is_available():
+        raise HipUnavailable("psrsigsim_amd computes on an MI355X (HIP) device; none is visible")
+    return L
+
+
+def last_error():
+    buf = ctypes.create_string_buffer(512)
+    load().pss_last_error(buf, 512)
+    return buf.value.decode(errors="replace")
+
+
+def check(rc, what=""):
+    if rc == PSS_OK:
+        return
+    msg = "%s: %s" % (what, last_error()) if what else last_error()
+    if rc == PSS_EINVAL:
+        raise ValueError(msg)
+    if rc == PSS_EUNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise RuntimeError(msg)

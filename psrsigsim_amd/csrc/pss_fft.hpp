@@ -1,0 +1,183 @@
+// pss_fft.hpp -- workgroup-level batched complex FFT for gfx950.
+//
+// Stockham autosort formulation (natural order in, natural order out, no bit
+// reversal), mixed radix, butterflies in registers, one LDS exchange between
+// stages.  A workgroup of T threads transforms BATCH sequences of length L;
+// every thread permanently holds E = L*BATCH/T complex values.
+//
+// Register mapping for a stage of radix R: value v[ib*R + q] (ib < E/R) is
+// element q of butterfly j = tid + ib*T, i.e. sequence b = j / (L/R) at
+// position jj + q*(L/R) with jj = j % (L/R).  On entry the first stage's
+// mapping must hold the INPUT positions; on exit the last stage's mapping holds
+// the OUTPUT positions (natural order).  Running the inverse with the reversed
+// radix list therefore starts from exactly the registers the forward left --
+// the row kernel fuses forward FFT -> ramp -> inverse FFT without touching LDS
+// in between.
+//
+// LDS layout: sequence b at row offset b*RS (RS = L + L/16 + 1 complex); inside
+// a row position p lives at p + (p >> 4).  The intra-row pad breaks the
+// stride-16 Stockham scatter; the odd row pitch breaks the cross-row transposes
+// of the column kernels (see DESIGN.md "LDS layout").
+#pragma once
+#include "pss_device.hpp"
+
+namespace pss {
+
+// cos/sin(2 pi k / 64), k = 0..63 (exactly 0/+-1 where the angle is a
+// multiple of pi/2).
+__device__ constexpr float kCos64[64] = {
+    1.0f, 0.99518472667219693f, 0.98078528040323043f, 0.95694033573220882f,
+    0.92387953251128674f, 0.88192126434835505f, 0.83146961230254524f, 0.77301045336273699f,
+    0.70710678118654757f, 0.63439328416364549f, 0.55557023301960229f, 0.47139673682599781f,
+    0.38268343236508984f, 0.29028467725446233f, 0.19509032201612833f, 0.098017140329560687f,
+    0.0f, -0.098017140329560576f, -0.19509032201612819f, -0.29028467725446222f,
+    -0.38268343236508973f, -0.4713967368259977f, -0.55557023301960196f, -0.63439328416364538f,
+    -0.70710678118654746f, -0.77301045336273699f, -0.83146961230254524f, -0.88192126434835494f,
+    -0.92387953251128674f, -0.95694033573220882f, -0.98078528040323043f, -0.99518472667219682f,
+    -1.0f, -0.99518472667219693f, -0.98078528040323043f, -0.95694033573220894f,
+    -0.92387953251128685f, -0.88192126434835505f, -0.83146961230254546f, -0.7730104533627371f,
+    -0.70710678118654768f, -0.63439328416364593f, -0.55557023301960218f, -0.47139673682599786f,
+    -0.38268343236509034f, -0.29028467725446244f, -0.19509032201612866f, -0.098017140329560798f,
+    0.0f, 0.098017140329560451f, 0.19509032201612803f, 0.29028467725446205f,
+    0.38268343236508967f, 0.47139673682599764f, 0.55557023301960196f, 0.63439328416364527f,
+    0.70710678118654746f, 0.77301045336273666f, 0.83146961230254501f, 0.88192126434835494f,
+    0.92387953251128652f, 0.95694033573220882f, 0.98078528040323032f, 0.99518472667219693f};
+
+// e^{-+2 pi i k/R} * x for compile-time-foldable k (forward uses the minus).
+template <int R, bool INV>
+__device__ __forceinline__ cf rot(int k, cf x) {
+    if (k == 0) return x;
+    if (4 * k == R) return INV ? make_float2(-x.y, x.x) : make_float2(x.y, -x.x);
+    const int idx = (k * (64 / R)) & 63;
+    const float c = kCos64[idx];
+    const float s = kCos64[(idx + 48) & 63];          // sin(a) = cos(a - pi/2)
+    const cf w = make_float2(c, INV ? s : -s);
+    return cmul(x, w);
+}
+
+// In-register DFT of a power-of-two size R (recursive radix-2 DIT; with full
+// unrolling every index and twiddle is a compile-time constant).
+template <int R, bool INV>
+__device__ __forceinline__ void dft(cf *a) {
+    if constexpr (R == 2) {
+        cf t = a[1];
+        a[1] = csub(a[0], t);
+        a[0] = cadd(a[0], t);
+    } else if constexpr (R > 2) {
+        constexpr int H = R / 2;
+        cf e[H], o[H];
+#pragma unroll
+        for (int i = 0; i < H; ++i) {
+            e[i] = a[2 * i];
+            o[i] = a[2 * i + 1];
+        }
+        dft<H, INV>(e);
+        dft<H, INV>(o);
+#pragma unroll
+        for (int k = 0; k < H; ++k) {
+            cf t = rot<R, INV>(k, o[k]);
+            a[k] = cadd(e[k], t);
+            a[k + H] = csub(e[k], t);
+        }
+    }
+}
+
+template <int L>
+struct Lds {
+    static constexpr int RS = L + L / 16 + 1;   // row pitch (complex)
+    __device__ static __forceinline__ int at(int b, int p) { return b * RS + p + (p >> 4); }
+    static constexpr int bytes(int batch) { return batch * RS * 8; }
+};
+
+template <int... Rs>
+struct RList {};
+
+template <int L, int BATCH, int T>
+struct Fft {
+    static constexpr int E = L * BATCH / T;
+    static_assert(E * T == L * BATCH, "T must divide L*BATCH");
+
+    // Fill registers with the first-stage INPUT mapping of radix R0 from LDS.
+    template <int R0>
+    __device__ static __forceinline__ void load(cf (&v)[E], const cf *lds, int tid) {
+        constexpr int LR = L / R0;
+#pragma unroll
+        for (int ib = 0; ib < E / R0; ++ib) {
+            const int j = tid + ib * T, b = j / LR, jj = j - b * LR;
+#pragma unroll
+            for (int q = 0; q < R0; ++q) v[ib * R0 + q] = lds[Lds<L>::at(b, jj + q * LR)];
+        }
+    }
+    // Store registers (last-stage OUTPUT mapping of radix R) to LDS, natural.
+    template <int R>
+    __device__ static __forceinline__ void store(const cf (&v)[E], cf *lds, int tid) {
+        constexpr int LR = L / R;
+#pragma unroll
+        for (int ib = 0; ib < E / R; ++ib) {
+            const int j = tid + ib * T, b = j / LR, jj = j - b * LR;
+#pragma unroll
+            for (int q = 0; q < R; ++q) lds[Lds<L>::at(b, jj + q * LR)] = v[ib * R + q];
+        }
+    }
+    // (b, position) of register i under the natural mapping of radix R.
+    template <int R>
+    __device__ static __forceinline__ void where(int i, int tid, int &b, int &pos) {
+        constexpr int LR = L / R;
+        const int ib = i / R, q = i - ib * R;
+        const int j = tid + ib * T;
+        b = j / LR;
+        pos = j - b * LR + q * LR;
+    }
+
+    // Run the stage list.  Ns = product of the radices already applied.
+    template <bool INV, int Ns, int R, int... Rest>
+    __device__ static __forceinline__ void run(cf (&v)[E], cf *lds, int tid) {
+        static_assert(E % R == 0, "E must be a multiple of every radix");
+        constexpr int LR = L / R;
+#pragma unroll
+        for (int ib = 0; ib < E / R; ++ib) {
+            const int j = tid + ib * T, b = j / LR, jj = j - b * LR;
+            const int k = jj % Ns;
+            cf *a = v + ib * R;
+            if constexpr (Ns > 1) {
+                // a[q] *= exp(-+2 pi i q k / (Ns R))   (exact rational angle)
+#pragma unroll
+                for (int q = 1; q < R; ++q) {
+                    int m = q * k;                       // < Ns*R <= L
+                    if (2 * m >= Ns * R) m -= Ns * R;    // [-1/2, 1/2) rev
+                    const float rev = (float)m * (1.0f / (float)(Ns * R));
+                    cf w = expi_rev(INV ? rev : -rev);
+                    a[q] = cmul(a[q], w);
+                }
+            }
+            dft<R, INV>(a);
+        }
+        if constexpr (sizeof...(Rest) > 0) {
+            // Stockham scatter of this stage's outputs, then gather the next
+            // stage's inputs.
+#pragma unroll
+            for (int ib = 0; ib < E / R; ++ib) {
+                const int j = tid + ib * T, b = j / LR, jj = j - b * LR;
+                const int k = jj % Ns;
+                const int base = (jj / Ns) * Ns * R + k;
+#pragma unroll
+                for (int q = 0; q < R; ++q) lds[Lds<L>::at(b, base + q * Ns)] = v[ib * R + q];
+            }
+            __syncthreads();
+            constexpr int R2 = first<Rest...>();
+            load<R2>(v, lds, tid);
+            __syncthreads();
+            run<INV, Ns * R, Rest...>(v, lds, tid);
+        }
+    }
+
+    template <int A, int... Z>
+    static constexpr int first() { return A; }
+    template <int... Z>
+    static constexpr int last_of() {
+        constexpr int a[] = {Z...};
+        return a[sizeof...(Z) - 1];
+    }
+};
+
+}  // namespace pss

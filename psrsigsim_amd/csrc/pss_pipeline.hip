@@ -1,0 +1,912 @@
+// pss_pipeline.hip -- fused filterbank synthesis engine for MI355X (gfx950).
+//
+// One PssPipeline run = source -> [FFT delay ramp] -> [null] -> [noise] -> data.
+// See include/pss_hip.h for the ABI and DESIGN.md for the kernel/roofline
+// discussion.  Paths:
+//   * no delay stage           : k_elementwise          (1 HBM pass)
+//   * N = 2^m, 64 <= N <= 8192 : k_single<L>            (1 HBM pass, FFT in LDS)
+//   * N = 2^m, N >= 16384      : k_colA -> k_row -> k_colC  (four-step, 2 spills)
+//   * any other even N         : direct DFT fallback    (O(N^2), correctness path)
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <math.h>
+
+#include "pss_device.hpp"
+#include "pss_fft.hpp"
+#include "../../include/pss_hip.h"
+
+using namespace pss;
+
+// ---------------------------------------------------------------------------
+// error reporting
+// ---------------------------------------------------------------------------
+static thread_local char g_err[512] = "";
+
+static int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIPCHK(x)                                                              \
+    do {                                                                       \
+        hipError_t e_ = (x);                                                   \
+        if (e_ != hipSuccess)                                                  \
+            return fail(PSS_EHIP, "%s: %s", #x, hipGetErrorString(e_));        \
+    } while (0)
+
+#define LAUNCHCHK()                                                            \
+    do {                                                                       \
+        hipError_t e_ = hipGetLastError();                                     \
+        if (e_ != hipSuccess)                                                  \
+            return fail(PSS_EHIP, "launch failed: %s", hipGetErrorString(e_)); \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// kernel parameters
+// ---------------------------------------------------------------------------
+struct KP {
+    PssPipeline p;
+    int64_t N;      // samples per row
+    int64_t N1;     // four-step: column length (1 for single-pass)
+    int64_t N2;     // four-step: row length    (N for single-pass)
+    float invN;
+};
+
+__device__ __forceinline__ int64_t floordiv(int64_t a, int64_t b) {
+    int64_t q = a / b;
+    if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+    return q;
+}
+
+// Box (nulled pulse) covering sample n, following the reference's numpy
+// indexing: bins = arange(Nph p, Nph (p+1)) + shift_val, filtered < N; negative
+// bins address from the end; later pulses in the choice list overwrite.
+__device__ __forceinline__ bool box_of(const KP &k, int64_t n, int &rank, int &j) {
+    const PssPipeline &p = k.p;
+    rank = -1;
+    const int64_t nph = p.nph;
+    int64_t q = n - p.null_shift;
+    int64_t s = floordiv(q, nph);
+    if (s >= 0 && s < p.null_slots) {
+        int r = p.null_rank[s];
+        if (r >= 0) { rank = r; j = (int)(q - s * nph); }
+    }
+    q = n - k.N - p.null_shift;          // the same sample reached by a negative bin
+    s = floordiv(q, nph);
+    if (s >= 0 && s < p.null_slots) {
+        int r = p.null_rank[s];
+        if (r > rank) { rank = r; j = (int)(q - s * nph); }
+    }
+    return rank >= 0;
+}
+
+__device__ __forceinline__ float box_value(const KP &k, int64_t n, int rank, int j) {
+    const PssPipeline &p = k.p;
+    if (p.inj_box) return p.inj_box[n];
+    Rng g(p.seed, p.call_null, P_BOX);
+    return chi2_general(g, (uint32_t)j, (uint32_t)rank, p.null_box_df) * p.null_box_scale;
+}
+
+// chi2 draws for 4 consecutive samples n0..n0+3 (n0 % 4 == 0) of channel c.
+// df == 1: one Philox block per 4 samples; otherwise Marsaglia-Tsang per sample.
+__device__ __forceinline__ void draw4(const Rng &g, int64_t n0, uint32_t c, float df, float (&x)[4]) {
+    if (df == 1.0f) {
+        float4 q = chi2_1x4(g.bits((uint32_t)(n0 >> 2), c, (uint32_t)(n0 >> 34)));
+        x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = chi2_general(g, (uint32_t)(n0 + i), c, df);
+    }
+}
+
+__device__ __forceinline__ float pchip_eval(const KP &k, int prow, int64_t n) {
+    const PssPipeline &p = k.p;
+    const uint64_t ph = (uint64_t)n * p.phase_step;               // 2^-64 cycles
+    uint64_t iv = __umul64hi(ph, (uint64_t)p.knot_m);             // interval index
+    const uint64_t uf = ph * (uint64_t)p.knot_m;                   // fraction in it
+    float u = (float)(uf >> 40) * 5.9604644775390625e-08f;         // * 2^-24
+    if (iv >= (uint64_t)p.nint) {                                  // extrapolate
+        u += (float)(iv - (uint64_t)(p.nint - 1));
+        iv = p.nint - 1;
+    }
+    const float4 cc = reinterpret_cast<const float4 *>(p.prof)[(int64_t)prow * p.nint + iv];
+    return fmaf(fmaf(fmaf(cc.x, u, cc.y), u, cc.z), u, cc.w);
+}
+
+// Source stage for 4 consecutive samples (cnt valid) of local row r.
+// re = data (generated or loaded, with an undelayed null applied);
+// im = delayed-null box mask (0 elsewhere).
+__device__ __forceinline__ void source4(const KP &k, int r, int64_t n0, int cnt,
+                                        float (&re)[4], float (&im)[4], bool want_re) {
+    const PssPipeline &p = k.p;
+    const uint32_t c = (uint32_t)(p.chan0 + r);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { re[i] = 0.f; im[i] = 0.f; }
+    if (want_re) {
+        if (p.src == PSS_SRC_LOAD) {
+            const float *row = p.data + (int64_t)r * p.ld;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) if (i < cnt) re[i] = row[n0 + i];
+        } else {
+            float x[4];
+            if (p.inj_gen) {
+                const float *row = p.inj_gen + (int64_t)r * k.N;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[i] = (i < cnt) ? row[n0 + i] : 0.f;
+            } else {
+                Rng g(p.seed, p.call_gen, P_PULSE);
+                draw4(g, n0, c, p.gen_df, x);
+            }
+            const int prow = (p.prof_rows == 1) ? 0 : (int)c;
+            if (p.src == PSS_SRC_SEARCH) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (i < cnt) re[i] = pchip_eval(k, prow, n0 + i) * x[i] * p.draw_norm;
+            } else {   // FOLD
+                const float *pr = p.prof + (int64_t)prow * p.nph;
+                uint32_t b = (uint32_t)(n0 % p.nph);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (i < cnt) re[i] = pr[b] * x[i] * p.draw_norm;
+                    if (++b == (uint32_t)p.nph) b = 0;
+                }
+            }
+        }
+        if (p.null_mode == PSS_NULL_UNDELAYED) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                int rk, j;
+                if (i < cnt && box_of(k, n0 + i, rk, j)) re[i] = box_value(k, n0 + i, rk, j);
+            }
+        }
+    }
+    if (p.null_mode == PSS_NULL_DELAYED) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            int rk, j;
+            if (i < cnt) {
+                if (p.inj_box) im[i] = p.inj_box[n0 + i];
+                else if (box_of(k, n0 + i, rk, j)) im[i] = box_value(k, n0 + i, rk, j);
+            }
+        }
+    }
+}
+
+// Epilogue for 4 consecutive samples: delayed-null replacement where the
+// shifted mask exceeds 1, the observe() pre-noise copy, radiometer noise, store.
+// `pre` holds the data value (FFT output already scaled by 1/N, or the source).
+__device__ __forceinline__ void epilogue4(const KP &k, int r, int64_t n0, int cnt,
+                                          float (&pre)[4], const float (&mask)[4], bool load_data) {
+    const PssPipeline &p = k.p;
+    const uint32_t c = (uint32_t)(p.chan0 + r);
+    float *row = p.data + (int64_t)r * p.ld;
+    if (load_data) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) if (i < cnt) pre[i] = row[n0 + i];
+    }
+    if (p.null_mode == PSS_NULL_DELAYED) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (i < cnt && mask[i] > 1.0f) {
+                if (p.inj_rep) {
+                    pre[i] = p.inj_rep[(int64_t)r * k.N + n0 + i];
+                } else {
+                    Rng g(p.seed, p.call_null, P_REP);
+                    pre[i] = chi2_general(g, (uint32_t)(n0 + i), c, p.null_rep_df) * p.null_rep_scale;
+                }
+            }
+        }
+    }
+    if (p.out_kind == PSS_OUT_F32) {
+        float *o = (float *)p.out + (int64_t)r * k.N;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) if (i < cnt) o[n0 + i] = (pre[i] > p.clip) ? p.clip : pre[i];
+    } else if (p.out_kind == PSS_OUT_I8) {
+        int8_t *o = (int8_t *)p.out + (int64_t)r * k.N;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (i < cnt) {
+                float v = (pre[i] > p.clip) ? p.clip : pre[i];
+                v = fminf(fmaxf(v, -128.f), 127.f);
+                o[n0 + i] = (int8_t)(int)truncf(v);
+            }
+        }
+    }
+    if (p.noise) {
+        float x[4];
+        if (p.inj_noise) {
+            const float *nr = p.inj_noise + (int64_t)r * k.N;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = (i < cnt) ? nr[n0 + i] : 0.f;
+        } else {
+            Rng g(p.seed, p.call_noise, P_NOISE);
+            draw4(g, n0, c, p.noise_df, x);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pre[i] = fmaf(p.noise_norm, x[i], pre[i]);
+    }
+    if (cnt == 4 && (((uintptr_t)(row + n0)) & 15) == 0) {
+        *reinterpret_cast<float4 *>(row + n0) = make_float4(pre[0], pre[1], pre[2], pre[3]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) if (i < cnt) row[n0 + i] = pre[i];
+    }
+}
+
+// exp(-2 pi i k' s / N) for frequency bin k, with the reference's Nyquist
+// rule applied separately to the real (data) and imaginary (mask) parts.
+__device__ __forceinline__ cf apply_ramp(const KP &k, int r, int64_t kb, cf z) {
+    const PssPipeline &p = k.p;
+    const int64_t N = k.N;
+    if (2 * kb == N) return make_float2(z.x * p.nyq_re[r], z.y * p.nyq_im[r]);
+    if (kb == 0) return z;
+    const int64_t kk = (2 * kb > N) ? kb - N : kb;
+    const uint64_t ph = (uint64_t)kk * p.ramp[r];
+    return cmul(z, expi_rev(-fix_to_rev(ph)));
+}
+
+// ---------------------------------------------------------------------------
+// path 0: no FFT -- source -> null(undelayed) -> epilogue, one pass
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_elementwise(KP k) {
+    const int r = blockIdx.y;
+    const int64_t items = (k.N + 3) >> 2;
+    for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < items;
+         it += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t n0 = it << 2;
+        const int cnt = (int)min((int64_t)4, k.N - n0);
+        float re[4], im[4];
+        source4(k, r, n0, cnt, re, im, true);
+        epilogue4(k, r, n0, cnt, re, im, false);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// path 1: whole row(s) in LDS.  BATCH rows of length L per workgroup.
+// ---------------------------------------------------------------------------
+template <int L, int BATCH, int T, typename FWD, typename INV>
+struct SinglePass;
+
+template <int L, int BATCH, int T, int... F, int... I>
+struct SinglePass<L, BATCH, T, RList<F...>, RList<I...>> {
+    using FF = Fft<L, BATCH, T>;
+    static constexpr int E = FF::E;
+    static constexpr int RF0 = FF::template first<F...>();
+    static constexpr int RFL = FF::template last_of<F...>();
+    static constexpr int RIL = FF::template last_of<I...>();
+
+    __device__ static void body(const KP &k) {
+        __shared__ cf lds[BATCH * Lds<L>::RS];
+        const int tid = threadIdx.x;
+        const int r0 = blockIdx.x * BATCH;
+        const PssPipeline &p = k.p;
+        const bool re_in = p.data_in_fft != 0;
+        // source -> LDS
+        for (int it = tid; it < BATCH * L / 4; it += T) {
+            const int b = it / (L / 4);
+            const int n0 = (it - b * (L / 4)) * 4;
+            float re[4], im[4];
+            if (r0 + b < p.nchan) source4(k, r0 + b, n0, 4, re, im, re_in);
+            else { for (int i = 0; i < 4; ++i) { re[i] = 0.f; im[i] = 0.f; } }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lds[Lds<L>::at(b, n0 + i)] = make_float2(re[i], im[i]);
+        }
+        __syncthreads();
+        cf v[E];
+        FF::template load<RF0>(v, lds, tid);
+        __syncthreads();
+        FF::template run<false, 1, F...>(v, lds, tid);
+        // ramp on natural-order spectrum (last forward stage mapping)
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+            int b, pos;
+            FF::template where<RFL>(i, tid, b, pos);
+            const int rr = min(r0 + b, p.nchan - 1);
+            v[i] = apply_ramp(k, rr, pos, v[i]);
+        }
+        FF::template run<true, 1, I...>(v, lds, tid);
+        FF::template store<RIL>(v, lds, tid);
+        __syncthreads();
+        for (int it = tid; it < BATCH * L / 4; it += T) {
+            const int b = it / (L / 4);
+            const int n0 = (it - b * (L / 4)) * 4;
+            if (r0 + b >= p.nchan) continue;
+            float pre[4], msk[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                cf z = lds[Lds<L>::at(b, n0 + i)];
+                pre[i] = z.x * k.invN;
+                msk[i] = z.y * k.invN;
+            }
+            epilogue4(k, r0 + b, n0, 4, pre, msk, !re_in);
+        }
+    }
+};
+
+template <typename SP, int T>
+__global__ __launch_bounds__(T) void k_single(KP k) { SP::body(k); }
+
+// ---------------------------------------------------------------------------
+// path 2: four-step, N = N1 * N2, sample n = N2*n1 + n2, bin k = k1 + N1*k2.
+//   A: per (row, block of B columns n2): source, FFT over n1, * W_N^{n2 k1},
+//      store Y[row][k1][n2]                                  (work, complex)
+//   B: per (row, BR rows k1): FFT over n2 -> ramp(k) -> inverse FFT over k2
+//   C: per (row, block of B columns n2): * W_N^{-k1 n2}, inverse FFT over k1,
+//      epilogue (null / out / noise), store data[row][N2*n1 + n2]
+// ---------------------------------------------------------------------------
+template <int N1, int B, int T, typename FWD, typename INV>
+struct Cols;
+
+template <int N1, int B, int T, int... F, int... I>
+struct Cols<N1, B, T, RList<F...>, RList<I...>> {
+    using FF = Fft<N1, B, T>;
+    static constexpr int E = FF::E;
+    static constexpr int RF0 = FF::template first<F...>();
+    static constexpr int RFL = FF::template last_of<F...>();
+    static constexpr int RI0 = FF::template first<I...>();
+    static constexpr int RIL = FF::template last_of<I...>();
+
+    __device__ static void passA(const KP &k) {
+        __shared__ cf lds[B * Lds<N1>::RS];
+        const int tid = threadIdx.x;
+        const int r = blockIdx.y;
+        const int64_t n20 = (int64_t)blockIdx.x * B;
+        const int64_t N2 = k.N2;
+        const bool re_in = k.p.data_in_fft != 0;
+        for (int it = tid; it < N1 * B / 4; it += T) {
+            const int n1 = it / (B / 4);
+            const int b4 = (it - n1 * (B / 4)) * 4;
+            float re[4], im[4];
+            source4(k, r, n1 * N2 + n20 + b4, 4, re, im, re_in);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lds[Lds<N1>::at(b4 + i, n1)] = make_float2(re[i], im[i]);
+        }
+        __syncthreads();
+        cf v[E];
+        FF::template load<RF0>(v, lds, tid);
+        __syncthreads();
+        FF::template run<false, 1, F...>(v, lds, tid);
+        const float invN = k.invN;
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+            int b, k1;
+            FF::template where<RFL>(i, tid, b, k1);
+            int64_t m = (n20 + b) * (int64_t)k1;          // < N
+            float rev = (float)m * invN;
+            if (rev >= 0.5f) rev -= 1.0f;
+            v[i] = cmul(v[i], expi_rev(-rev));
+        }
+        FF::template store<RFL>(v, lds, tid);
+        __syncthreads();
+        cf *Y = reinterpret_cast<cf *>(k.p.work) + (int64_t)r * k.N;
+        for (int it = tid; it < N1 * B / 4; it += T) {
+            const int k1 = it / (B / 4);
+            const int b4 = (it - k1 * (B / 4)) * 4;
+            cf a0 = lds[Lds<N1>::at(b4 + 0, k1)], a1 = lds[Lds<N1>::at(b4 + 1, k1)];
+            cf a2 = lds[Lds<N1>::at(b4 + 2, k1)], a3 = lds[Lds<N1>::at(b4 + 3, k1)];
+            float4 *dst = reinterpret_cast<float4 *>(Y + (int64_t)k1 * N2 + n20 + b4);
+            dst[0] = make_float4(a0.x, a0.y, a1.x, a1.y);
+            dst[1] = make_float4(a2.x, a2.y, a3.x, a3.y);
+        }
+    }
+
+    __device__ static void passC(const KP &k) {
+        __shared__ cf lds[B * Lds<N1>::RS];
+        const int tid = threadIdx.x;
+        const int r = blockIdx.y;
+        const int64_t n20 = (int64_t)blockIdx.x * B;
+        const int64_t N2 = k.N2;
+        const float invN = k.invN;
+        const cf *Y = reinterpret_cast<const cf *>(k.p.work) + (int64_t)r * k.N;
+        for (int it = tid; it < N1 * B / 4; it += T) {
+            const int k1 = it / (B / 4);
+            const int b4 = (it - k1 * (B / 4)) * 4;
+            const float4 *src = reinterpret_cast<const float4 *>(Y + (int64_t)k1 * N2 + n20 + b4);
+            float4 lo = src[0], hi = src[1];
+            cf a[4] = {make_float2(lo.x, lo.y), make_float2(lo.z, lo.w),
+                       make_float2(hi.x, hi.y), make_float2(hi.z, hi.w)};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                int64_t m = (n20 + b4 + i) * (int64_t)k1;
+                float rev = (float)m * invN;
+                if (rev >= 0.5f) rev -= 1.0f;
+                lds[Lds<N1>::at(b4 + i, k1)] = cmul(a[i], expi_rev(rev));
+            }
+        }
+        __syncthreads();
+        cf v[E];
+        FF::template load<RI0>(v, lds, tid);
+        __syncthreads();
+        FF::template run<true, 1, I...>(v, lds, tid);
+        FF::template store<RIL>(v, lds, tid);
+        __syncthreads();
+        const bool re_in = k.p.data_in_fft != 0;
+        for (int it = tid; it < N1 * B / 4; it += T) {
+            const int n1 = it / (B / 4);
+            const int b4 = (it - n1 * (B / 4)) * 4;
+            float pre[4], msk[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                cf z = lds[Lds<N1>::at(b4 + i, n1)];
+                pre[i] = z.x * invN;
+                msk[i] = z.y * invN;
+            }
+            epilogue4(k, r, n1 * N2 + n20 + b4, 4, pre, msk, !re_in);
+        }
+    }
+};
+
+template <typename C, int T>
+__global__ __launch_bounds__(T) void k_colA(KP k) { C::passA(k); }
+template <typename C, int T>
+__global__ __launch_bounds__(T) void k_colC(KP k) { C::passC(k); }
+
+template <int N2, int BR, int T, typename FWD, typename INV>
+struct Rows;
+
+template <int N2, int BR, int T, int... F, int... I>
+struct Rows<N2, BR, T, RList<F...>, RList<I...>> {
+    using FF = Fft<N2, BR, T>;
+    static constexpr int E = FF::E;
+    static constexpr int RF0 = FF::template first<F...>();
+    static constexpr int RFL = FF::template last_of<F...>();
+    static constexpr int RIL = FF::template last_of<I...>();
+    static_assert(RIL == RF0, "inverse plan must be the reversed forward plan");
+
+    __device__ static void pass(const KP &k) {
+        __shared__ cf lds[BR * Lds<N2>::RS];
+        const int tid = threadIdx.x;
+        const int r = blockIdx.y;
+        const int64_t k10 = (int64_t)blockIdx.x * BR;
+        cf *Y = reinterpret_cast<cf *>(k.p.work) + (int64_t)r * k.N + k10 * N2;
+        cf v[E];
+        constexpr int LR = N2 / RF0;
+#pragma unroll
+        for (int ib = 0; ib < E / RF0; ++ib) {
+            const int j = tid + ib * T, b = j / LR, jj = j - b * LR;
+#pragma unroll
+            for (int q = 0; q < RF0; ++q) v[ib * RF0 + q] = Y[(int64_t)b * N2 + jj + q * LR];
+        }
+        FF::template run<false, 1, F...>(v, lds, tid);
+        const int64_t N1 = k.N1;
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+            int b, k2;
+            FF::template where<RFL>(i, tid, b, k2);
+            v[i] = apply_ramp(k, r, k10 + b + N1 * (int64_t)k2, v[i]);
+        }
+        __syncthreads();   // LDS reuse by the inverse's first exchange
+        FF::template run<true, 1, I...>(v, lds, tid);
+#pragma unroll
+        for (int ib = 0; ib < E / RF0; ++ib) {
+            const int j = tid + ib * T, b = j / LR, jj = j - b * LR;
+#pragma unroll
+            for (int q = 0; q < RF0; ++q) Y[(int64_t)b * N2 + jj + q * LR] = v[ib * RF0 + q];
+        }
+    }
+};
+
+template <typename R, int T>
+__global__ __launch_bounds__(T) void k_row(KP k) { R::pass(k); }
+
+// ---------------------------------------------------------------------------
+// path 3: direct DFT fallback for even N that are not handled above.
+//   W1[row][n] = source (complex), W2[row][k] = DFT(W1) * ramp, then inverse
+//   DFT + epilogue.  O(N^2); LDS-tiled over the summation index.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fb_source(KP k) {
+    const int r = blockIdx.y;
+    cf *W1 = reinterpret_cast<cf *>(k.p.work) + (int64_t)r * k.N;
+    const int64_t items = (k.N + 3) >> 2;
+    const bool re_in = k.p.data_in_fft != 0;
+    for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < items;
+         it += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t n0 = it << 2;
+        const int cnt = (int)min((int64_t)4, k.N - n0);
+        float re[4], im[4];
+        source4(k, r, n0, cnt, re, im, re_in);
+        for (int i = 0; i < cnt; ++i) W1[n0 + i] = make_float2(re[i], im[i]);
+    }
+}
+
+// exp(-2 pi i m / N) for m in [0, N), double-precision angles (fallback path)
+__global__ void k_fb_twiddles(KP k) {
+    cf *tw = reinterpret_cast<cf *>(k.p.work) + (int64_t)2 * k.p.nchan * k.N;
+    for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < k.N;
+         m += (int64_t)gridDim.x * blockDim.x) {
+        double s, c;
+        sincospi(-2.0 * (double)m / (double)k.N, &s, &c);
+        tw[m] = make_float2((float)c, (float)s);
+    }
+}
+
+template <bool INV>
+__global__ __launch_bounds__(256) void k_fb_dft(KP k) {
+    __shared__ cf tile[1024];
+    const int r = blockIdx.y;
+    const int64_t N = k.N;
+    const cf *in = reinterpret_cast<const cf *>(k.p.work) + (int64_t)(INV ? k.p.nchan + r : r) * N;
+    const cf *tw = reinterpret_cast<const cf *>(k.p.work) + (int64_t)2 * k.p.nchan * N;
+    const int64_t kout = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double accr = 0.0, acci = 0.0;
+    // twiddle index m = (kout * n) mod N, advanced incrementally (exact)
+    const int64_t kk = kout < N ? kout : 0;
+    for (int64_t base = 0; base < N; base += 1024) {
+        const int cnt = (int)min((int64_t)1024, N - base);
+        __syncthreads();
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x) tile[i] = in[base + i];
+        __syncthreads();
+        int64_t m = (kk * base) % N;
+        for (int i = 0; i < cnt; ++i) {
+            cf w = tw[m];
+            if (INV) w.y = -w.y;
+            const cf x = tile[i];
+            accr += (double)x.x * w.x - (double)x.y * w.y;
+            acci += (double)x.x * w.y + (double)x.y * w.x;
+            m += kk;
+            if (m >= N) m -= N;
+        }
+    }
+    if (kout >= N) return;
+    if (!INV) {
+        cf z = apply_ramp(k, r, kout, make_float2((float)accr, (float)acci));
+        reinterpret_cast<cf *>(k.p.work)[(int64_t)(k.p.nchan + r) * N + kout] = z;
+    } else {
+        // stash the inverse result in W1 (no longer needed) for the epilogue
+        reinterpret_cast<cf *>(k.p.work)[(int64_t)r * N + kout] =
+            make_float2((float)(accr / (double)N), (float)(acci / (double)N));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fb_epilogue(KP k) {
+    const int r = blockIdx.y;
+    const cf *W1 = reinterpret_cast<const cf *>(k.p.work) + (int64_t)r * k.N;
+    const int64_t items = (k.N + 3) >> 2;
+    const bool re_in = k.p.data_in_fft != 0;
+    for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < items;
+         it += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t n0 = it << 2;
+        const int cnt = (int)min((int64_t)4, k.N - n0);
+        float pre[4] = {0, 0, 0, 0}, msk[4] = {0, 0, 0, 0};
+        for (int i = 0; i < cnt; ++i) { pre[i] = W1[n0 + i].x; msk[i] = W1[n0 + i].y; }
+        epilogue4(k, r, n0, cnt, pre, msk, !re_in);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// utility kernels
+// ---------------------------------------------------------------------------
+__global__ void k_down_sample(const float *in, float *out, int64_t in_len, int64_t in_ld,
+                              int32_t fact) {
+    const int r = blockIdx.y;
+    const int64_t nout = in_len / fact;
+    const float *row = in + (int64_t)r * in_ld;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nout;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        double s = 0.0;
+        for (int j = 0; j < fact; ++j) s += row[i * fact + j];
+        out[(int64_t)r * nout + i] = (float)(s / fact);
+    }
+}
+
+__global__ void k_rebin(const float *in, float *out, int64_t in_ld, int32_t newlen,
+                        const int64_t *lo, const int64_t *hi) {
+    const int r = blockIdx.y;
+    const float *row = in + (int64_t)r * in_ld;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < newlen; i += gridDim.x * blockDim.x) {
+        double s = 0.0;
+        const int64_t a = lo[i], b = hi[i];
+        for (int64_t j = a; j < b; ++j) s += row[j];
+        out[(int64_t)r * newlen + i] = (b > a) ? (float)(s / (double)(b - a)) : NAN;
+    }
+}
+
+__global__ void k_clip_cast(const float *in, void *out, int64_t count, float clip, int32_t kind) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        float v = in[i];
+        v = (v > clip) ? clip : v;
+        if (kind == PSS_OUT_F32) {
+            ((float *)out)[i] = v;
+        } else {
+            v = fminf(fmaxf(v, -128.f), 127.f);
+            ((int8_t *)out)[i] = (int8_t)(int)truncf(v);
+        }
+    }
+}
+
+__global__ void k_fold(const float *data, float *out, int64_t ld, int64_t npbins, int64_t n_fold) {
+    const int c = blockIdx.y;
+    const int64_t half = npbins / 2;
+    const float *row = data + (int64_t)c * ld + npbins;
+    for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < half;
+         b += (int64_t)gridDim.x * blockDim.x) {
+        double s = 0.0;
+        for (int64_t f = 0; f < n_fold; ++f) s += row[f * half + b];
+        out[(int64_t)c * half + b] = (float)s;
+    }
+}
+
+__global__ void k_chi2_fill(float *out, int64_t n, int32_t chan0, float df, uint64_t seed,
+                            uint32_t call_id, uint32_t purpose) {
+    const int r = blockIdx.y;
+    Rng g(seed, call_id, purpose);
+    const int64_t items = (n + 3) >> 2;
+    for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < items;
+         it += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t n0 = it << 2;
+        float x[4];
+        draw4(g, n0, (uint32_t)(chan0 + r), df, x);
+        for (int i = 0; i < 4 && n0 + i < n; ++i) out[(int64_t)r * n + n0 + i] = x[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host dispatch
+// ---------------------------------------------------------------------------
+static inline bool is_pow2(int64_t n) { return n > 0 && (n & (n - 1)) == 0; }
+
+static dim3 stream_grid(int64_t items, int rows) {
+    int64_t bx = (items + 255) / 256;
+    if (bx > 4096) bx = 4096;
+    if (bx < 1) bx = 1;
+    return dim3((unsigned)bx, (unsigned)rows, 1);
+}
+
+
+template <int L, int BATCH, int T, typename F, typename I>
+static int launch_single(const KP &k, hipStream_t st) {
+    using SP = SinglePass<L, BATCH, T, F, I>;
+    dim3 grid((k.p.nchan + BATCH - 1) / BATCH);
+    k_single<SP, T><<<grid, dim3(T), 0, st>>>(k);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+template <int N1, int B, int T, typename CF, typename CI, int N2, int BR, int TR, typename RF, typename RI>
+static int launch_four(const KP &k, hipStream_t st) {
+    using C = Cols<N1, B, T, CF, CI>;
+    using R = Rows<N2, BR, TR, RF, RI>;
+    dim3 gc((unsigned)(N2 / B), (unsigned)k.p.nchan);
+    k_colA<C, T><<<gc, dim3(T), 0, st>>>(k);
+    LAUNCHCHK();
+    dim3 gr((unsigned)(N1 / BR), (unsigned)k.p.nchan);
+    k_row<R, TR><<<gr, dim3(TR), 0, st>>>(k);
+    LAUNCHCHK();
+    k_colC<C, T><<<gc, dim3(T), 0, st>>>(k);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+// Column plans: B*N1 = 8192 complex per workgroup, 512 threads, 16 per thread.
+// Row plans: N2 = 8192 (1 row, 512 thr) or N2 <= 4096 (4096/N2 rows, 256 thr).
+using C16 = RList<16>;
+using C32F = RList<16, 2>;
+using C32I = RList<2, 16>;
+using C64F = RList<16, 4>;
+using C64I = RList<4, 16>;
+using C128F = RList<16, 8>;
+using C128I = RList<8, 16>;
+using C256 = RList<16, 16>;
+using C512F = RList<16, 16, 2>;
+using C512I = RList<2, 16, 16>;
+using C1kF = RList<16, 16, 4>;
+using C1kI = RList<4, 16, 16>;
+using C2kF = RList<16, 16, 8>;
+using C2kI = RList<8, 16, 16>;
+using C4k = RList<16, 16, 16>;
+using C8kF = RList<16, 16, 16, 2>;
+using C8kI = RList<2, 16, 16, 16>;
+
+static int run_fourstep(KP &k, hipStream_t st) {
+    const int64_t N = k.N;
+    if (N >= (1 << 17)) {
+        k.N2 = 8192;
+        k.N1 = N / 8192;
+        switch (k.N1) {
+#define CASE8K(N1_, CF, CI)                                                                      \
+    case N1_:                                                                                    \
+        return launch_four<N1_, 8192 / N1_, 512, CF, CI, 8192, 1, 512, C8kF, C8kI>(k, st);
+            CASE8K(16, C16, C16)
+            CASE8K(32, C32F, C32I)
+            CASE8K(64, C64F, C64I)
+            CASE8K(128, C128F, C128I)
+            CASE8K(256, C256, C256)
+            CASE8K(512, C512F, C512I)
+            CASE8K(1024, C1kF, C1kI)
+            CASE8K(2048, C2kF, C2kI)
+#undef CASE8K
+            default: break;
+        }
+        return fail(PSS_EUNSUPPORTED, "four-step: N=%lld too large", (long long)N);
+    }
+    // 2^14 .. 2^16: N1 = 16 columns, rows of N/16
+    k.N1 = 16;
+    k.N2 = N / 16;
+    switch (k.N2) {
+        case 1024:
+            return launch_four<16, 512, 512, C16, C16, 1024, 4, 256, C1kF, C1kI>(k, st);
+        case 2048:
+            return launch_four<16, 512, 512, C16, C16, 2048, 2, 256, C2kF, C2kI>(k, st);
+        case 4096:
+            return launch_four<16, 512, 512, C16, C16, 4096, 1, 256, C4k, C4k>(k, st);
+        default: break;
+    }
+    return fail(PSS_EUNSUPPORTED, "four-step: N=%lld", (long long)N);
+}
+
+static int run_single(KP &k, hipStream_t st) {
+    k.N1 = 1;
+    k.N2 = k.N;
+    switch (k.N) {
+        case 64: return launch_single<64, 64, 256, C64F, C64I>(k, st);
+        case 128: return launch_single<128, 32, 256, C128F, C128I>(k, st);
+        case 256: return launch_single<256, 16, 256, C256, C256>(k, st);
+        case 512: return launch_single<512, 8, 256, C512F, C512I>(k, st);
+        case 1024: return launch_single<1024, 4, 256, C1kF, C1kI>(k, st);
+        case 2048: return launch_single<2048, 2, 256, C2kF, C2kI>(k, st);
+        case 4096: return launch_single<4096, 1, 256, C4k, C4k>(k, st);
+        case 8192: return launch_single<8192, 1, 512, C8kF, C8kI>(k, st);
+        default: break;
+    }
+    return fail(PSS_EUNSUPPORTED, "single-pass: N=%lld", (long long)k.N);
+}
+
+static int run_fallback(KP &k, hipStream_t st) {
+    dim3 g = stream_grid((k.N + 3) / 4, k.p.nchan);
+    k_fb_source<<<g, dim3(256), 0, st>>>(k);
+    LAUNCHCHK();
+    k_fb_twiddles<<<stream_grid(k.N, 1), dim3(256), 0, st>>>(k);
+    LAUNCHCHK();
+    dim3 gd((unsigned)((k.N + 255) / 256), (unsigned)k.p.nchan);
+    k_fb_dft<false><<<gd, dim3(256), 0, st>>>(k);
+    LAUNCHCHK();
+    k_fb_dft<true><<<gd, dim3(256), 0, st>>>(k);
+    LAUNCHCHK();
+    k_fb_epilogue<<<g, dim3(256), 0, st>>>(k);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+extern "C" int64_t pss_workspace_bytes(int32_t nchan, int64_t nsamp);
+
+static int validate(const PssPipeline *p) {
+    if (!p) return fail(PSS_EINVAL, "null pipeline");
+    if (p->nchan <= 0 || p->nsamp <= 0) return fail(PSS_EINVAL, "empty signal (%d x %lld)", p->nchan, (long long)p->nsamp);
+    if (p->nchan > 65535) return fail(PSS_EINVAL, "nchan %d > 65535 per launch", p->nchan);
+    if (!p->data) return fail(PSS_EINVAL, "data is NULL");
+    if (p->ld < p->nsamp) return fail(PSS_EINVAL, "ld < nsamp");
+    if (p->src == PSS_SRC_SEARCH && (!p->prof || p->nint < 1 || p->knot_m < 1))
+        return fail(PSS_EINVAL, "search source needs a PCHIP table");
+    if (p->src == PSS_SRC_FOLD && (!p->prof || p->nph < 1))
+        return fail(PSS_EINVAL, "fold source needs a profile table");
+    if (p->null_mode != PSS_NULL_NONE && (!p->null_rank || p->nph < 1))
+        return fail(PSS_EINVAL, "null needs null_rank and nph");
+    if (p->null_mode == PSS_NULL_DELAYED && !p->shift)
+        return fail(PSS_EINVAL, "delayed null needs the FFT delay stage");
+    if (p->shift) {
+        if (p->nsamp & 1)
+            return fail(PSS_EINVAL, "odd N=%lld: the reference's irfft returns N-1 samples", (long long)p->nsamp);
+        if (!p->ramp || !p->nyq_re || !p->nyq_im) return fail(PSS_EINVAL, "shift needs ramp/nyq arrays");
+        if (!p->work && pss_workspace_bytes(p->nchan, p->nsamp) > 0)
+            return fail(PSS_EINVAL, "shift needs a workspace");
+        if (p->nsamp > (1ll << 24) && !is_pow2(p->nsamp))
+            return fail(PSS_EUNSUPPORTED, "N=%lld", (long long)p->nsamp);
+    }
+    if (p->out_kind != PSS_OUT_NONE && !p->out) return fail(PSS_EINVAL, "out is NULL");
+    return PSS_OK;
+}
+
+extern "C" {
+
+int pss_version(void) { return 100; }
+
+int pss_last_error(char *buf, size_t n) {
+    if (buf && n) {
+        strncpy(buf, g_err, n - 1);
+        buf[n - 1] = 0;
+    }
+    return (int)strlen(g_err);
+}
+
+int64_t pss_workspace_bytes(int32_t nchan, int64_t nsamp) {
+    const int64_t one = (int64_t)nchan * nsamp * 8;
+    if (is_pow2(nsamp) && nsamp >= 64 && nsamp <= (1ll << 24)) return nsamp > 8192 ? one : 0;
+    return 2 * one + nsamp * 8;   // fallback: W1, W2 and the twiddle table
+}
+
+int pss_run(const PssPipeline *p, void *stream) {
+    int rc = validate(p);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    KP k;
+    k.p = *p;
+    k.N = p->nsamp;
+    k.N1 = 1;
+    k.N2 = p->nsamp;
+    k.invN = (float)(1.0 / (double)p->nsamp);
+    if (!p->shift) {
+        dim3 g = stream_grid((k.N + 3) / 4, p->nchan);
+        k_elementwise<<<g, dim3(256), 0, st>>>(k);
+        LAUNCHCHK();
+        return PSS_OK;
+    }
+    const int64_t N = p->nsamp;
+    if (is_pow2(N) && N >= 64 && N <= 8192) return run_single(k, st);
+    if (is_pow2(N) && N >= 16384 && N <= (1ll << 24)) return run_fourstep(k, st);
+    return run_fallback(k, st);
+}
+
+int pss_shift_rows(float *rows, int32_t nrows, int64_t n, int64_t ld, const uint64_t *ramp,
+                   const float *nyq, void *work, void *stream) {
+    PssPipeline p;
+    memset(&p, 0, sizeof(p));
+    p.nchan = nrows;
+    p.nsamp = n;
+    p.ld = ld;
+    p.data = rows;
+    p.work = work;
+    p.src = PSS_SRC_LOAD;
+    p.shift = 1;
+    p.data_in_fft = 1;
+    p.ramp = ramp;
+    p.nyq_re = nyq;
+    p.nyq_im = nyq;
+    return pss_run(&p, stream);
+}
+
+int pss_down_sample(const float *in, float *out, int32_t nrows, int64_t in_len, int64_t in_ld,
+                    int32_t fact, void *stream) {
+    if (fact < 1 || in_len % fact) return fail(PSS_EINVAL, "down_sample: %lld %% %d != 0", (long long)in_len, fact);
+    if (nrows <= 0) return PSS_OK;
+    dim3 g = stream_grid(in_len / fact, nrows);
+    hipLaunchKernelGGL(k_down_sample, g, dim3(256), 0, (hipStream_t)stream, in, out, in_len, in_ld, fact);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+int pss_rebin(const float *in, float *out, int32_t nrows, int64_t in_len, int64_t in_ld, int32_t newlen,
+              const int64_t *lo, const int64_t *hi, void *stream) {
+    (void)in_len;
+    if (nrows <= 0 || newlen <= 0) return PSS_OK;
+    dim3 g = stream_grid(newlen, nrows);
+    hipLaunchKernelGGL(k_rebin, g, dim3(256), 0, (hipStream_t)stream, in, out, in_ld, newlen, lo, hi);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+int pss_clip_cast(const float *in, void *out, int64_t count, float clip, int32_t out_kind, void *stream) {
+    if (out_kind != PSS_OUT_F32 && out_kind != PSS_OUT_I8) return fail(PSS_EINVAL, "out_kind");
+    if (count <= 0) return PSS_OK;
+    dim3 g = stream_grid(count, 1);
+    hipLaunchKernelGGL(k_clip_cast, g, dim3(256), 0, (hipStream_t)stream, in, out, count, clip, out_kind);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+int pss_fold(const float *data, float *out, int32_t nchan, int64_t ld, int64_t npbins, int64_t n_fold,
+             void *stream) {
+    if (nchan <= 0 || npbins < 2) return fail(PSS_EINVAL, "fold geometry");
+    dim3 g = stream_grid(npbins / 2, nchan);
+    hipLaunchKernelGGL(k_fold, g, dim3(256), 0, (hipStream_t)stream, data, out, ld, npbins, n_fold);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+int pss_chi2_fill(float *out, int32_t nrows, int32_t chan0, int64_t n, float df, uint64_t seed,
+                  uint32_t call_id, uint32_t purpose, void *stream) {
+    if (nrows <= 0 || n <= 0) return PSS_OK;
+    dim3 g = stream_grid((n + 3) / 4, nrows);
+    hipLaunchKernelGGL(k_chi2_fill, g, dim3(256), 0, (hipStream_t)stream, out, n, chan0, df, seed,
+                       call_id, purpose);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+}  // extern "C"

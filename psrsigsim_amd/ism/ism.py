@@ -1,0 +1,136 @@
+"""ISM -- mirrors ``psrsigsim/ism/ism.py``.
+
+Every delay method computes its per-channel delays on the host (float64, the
+reference's formulas), accumulates ``signal._delay`` exactly as the reference
+does, and appends a delay stage to the signal's pending pipeline.  Consecutive
+delay stages run as ONE forward/inverse FFT pass on the GPU (the reference runs
+one rfft/irfft pair per channel per call: ism.py:57-60, 136-139, 203-206).
+"""
+import numpy as np
+
+from ..utils.constants import DM_K_VALUE, KOLMOGOROV_BETA
+from ..utils.utils import make_quant
+from .._units import Quantity, to_value
+from ..pulsar.portraits import DataPortrait
+from .. import _engine
+
+__all__ = ["ISM"]
+
+
+def push_delay(signal, delays_ms):
+    """Accumulate ``signal._delay`` (ms, ism.py:44-47) and append a delay
+    stage of delays_ms / dt samples per channel."""
+    delays_ms = np.asarray(delays_ms, dtype=np.float64)
+    if signal.delay is None:
+        signal._delay = Quantity(delays_ms.copy(), 'ms')
+    else:
+        signal._delay = Quantity(np.asarray(to_value(signal.delay, 'ms')) + delays_ms, 'ms')
+    if signal._ncols % 2:
+        # shift_t's irfft (no n=) returns N-1 samples; the row assignment fails
+        raise ValueError("could not broadcast input array from shape (%d,) into shape (%d,)"
+                         % (signal._ncols - 1, signal._ncols))
+    pend = signal._pending
+    if pend is not None and (pend.null is not None or pend.noise is not None):
+        signal._flush()
+        pend = None
+    if pend is None:
+        pend = signal._pend()
+    pend.shifts.append(delays_ms / signal._dt_ms())
+
+
+class ISM(object):
+    """ism.py:12-358 (filterbank path)."""
+
+    def __init__(self):
+        pass
+
+    def disperse(self, signal, dm):
+        """ism.py:20-38: cold-plasma delay DM_K * DM / f^2 per channel (f =
+        channel lower edge), relative to infinite frequency."""
+        signal._dm = make_quant(dm, 'pc/cm^3')
+        if hasattr(signal, '_dispersed'):
+            raise ValueError('Signal has already been dispersed!')
+        if signal.sigtype == 'FilterBankSignal':
+            self._disperse_filterbank(signal, signal._dm)
+        elif signal.sigtype == 'BasebandSignal':
+            self._disperse_baseband(signal, signal._dm)
+        signal._dispersed = True
+
+    def _disperse_filterbank(self, signal, dm):
+        """ism.py:40-74; delays in ms."""
+        f = signal._freqs_MHz()
+        delays_ms = (DM_K_VALUE * float(to_value(dm, 'pc/cm^3')) * np.power(f, -2.0)) * 1e3
+        push_delay(signal, delays_ms)
+
+    def _disperse_baseband(self, signal, dm):
+        raise NotImplementedError("baseband coherent dispersion is outside the filterbank path")
+
+    def FD_shift(self, signal, FD_params):
+        """ism.py:100-156: sum_i FD_i * ln(f / 1 GHz)^(i+1)."""
+        f = signal._freqs_MHz()
+        delays = np.zeros(len(f))
+        for ii in range(len(FD_params)):
+            c_ms = float(to_value(make_quant(FD_params[ii], 's'), 's')) * 1e3
+            delays += c_ms * np.power(np.log(f / 1000.0), ii + 1)
+        push_delay(signal, delays)
+        signal._FDshifted = True
+
+    def scatter_broaden(self, signal, tau_d, ref_freq, beta=KOLMOGOROV_BETA, convolve=False,
+                        pulsar=None):
+        """ism.py:158-240.  convolve=False: a pure extra delay
+        tau_d (f/f_ref)^(-2 beta/(beta-2)); convolve=True: linear convolution
+        of each channel's profile with a normalised exp(-t/tau) tail (before
+        make_pulses), replacing the pulsar's profile by a DataPortrait."""
+        f = signal._freqs_MHz()
+        ref = float(to_value(make_quant(ref_freq, 'MHz'), 'MHz'))
+        tau_ms = float(to_value(make_quant(tau_d, 's'), 's')) * 1e3
+        tau_scaled = self.scale_tau_d(tau_ms, ref, f, beta=beta)
+        if not convolve:
+            push_delay(signal, tau_scaled)
+            return
+        Nph = pulsar._nph(signal)
+        pulsar.Profiles.init_profiles(Nph, signal.Nchan)
+        full_profs = pulsar.Profiles.calc_profiles(np.linspace(0.0, 1.0, Nph), signal.Nchan)
+        t = np.linspace(0, pulsar._P(), Nph)
+        tails = np.zeros((signal.Nchan, Nph))
+        for ii, tau in enumerate(np.atleast_1d(tau_scaled)):
+            tails[ii, :] = np.exp(-t * 1e3 / tau)        # t [s] / tau [ms]
+        pulsar._Profiles = DataPortrait(self.convolve_profile(full_profs, tails, width=Nph))
+
+    def convolve_profile(self, profiles, convolve_array, width=2048):
+        """ism.py:243-288: per row, linear convolution of the sum-normalised
+        profile with the sum-normalised kernel, first `width` samples,
+        rescaled by the profile sum."""
+        for ii in range(convolve_array.shape[0]):
+            ps = np.sum(profiles[ii, :])
+            pn = profiles[ii, :] / ps if ps != 0.0 else profiles[ii, :]
+            ks = np.sum(convolve_array[ii, :])
+            kn = convolve_array[ii, :] / ks if ks != 0.0 else convolve_array[ii, :]
+            n = pn.size + kn.size - 1
+            conv = np.fft.irfft(np.fft.rfft(pn, n) * np.fft.rfft(kn, n), n)
+            profiles[ii, :] = ps * conv[:width]
+        return profiles
+
+    def scale_dnu_d(self, dnu_d, nu_i, nu_f, beta=KOLMOGOROV_BETA):
+        """ism.py:300-318."""
+        if beta < 4:
+            exp = 2.0 * beta / (beta - 2)
+        elif beta > 4:
+            exp = 8.0 / (6 - beta)
+        return dnu_d * (nu_f / nu_i) ** exp
+
+    def scale_dt_d(self, dt_d, nu_i, nu_f, beta=KOLMOGOROV_BETA):
+        """ism.py:320-338."""
+        if beta < 4:
+            exp = 2.0 / (beta - 2)
+        elif beta > 4:
+            exp = float(beta - 2) / (6 - beta)
+        return dt_d * (nu_f / nu_i) ** exp
+
+    def scale_tau_d(self, tau_d, nu_i, nu_f, beta=KOLMOGOROV_BETA):
+        """ism.py:340-358."""
+        if beta < 4:
+            exp = -2.0 * beta / (beta - 2)
+        elif beta > 4:
+            exp = -8.0 / (6 - beta)
+        return tau_d * (nu_f / nu_i) ** exp

@@ -1,0 +1,269 @@
+"""Pulse portraits (host plan layer).
+
+Mirrors ``psrsigsim/pulsar/portraits.py`` (class names, methods, the Amax /
+_max_profile state machine, errors).  Portraits are small (Nchan x Nph) float64
+tables built on the host; the per-sample evaluation over the whole
+(Nchan, nsamp) signal happens on the GPU (k_* source stage, ``pchip_eval``)
+from the PCHIP coefficient table exported by :meth:`DataPortrait.device_table`.
+
+The PCHIP construction follows the published Fritsch-Butland/Fritsch-Carlson
+monotone cubic (as in scipy.interpolate.PchipInterpolator, which the
+reference uses at portraits.py:252): weighted-harmonic-mean interior slopes,
+one-sided three-point end slopes with the shape-preserving clamps, cubic
+Hermite pieces, extrapolation with the end pieces.
+"""
+import logging
+
+import numpy as np
+
+log = logging.getLogger("psrsigsim_amd")
+
+__all__ = ["PulsePortrait", "GaussPortrait", "DataPortrait", "UserPortrait",
+           "pchip_slopes", "pchip_coefficients", "ppoly_eval"]
+
+
+# ---------------------------------------------------------------------------
+# PCHIP (float64, host)
+# ---------------------------------------------------------------------------
+def _edge_slope(h0, h1, m0, m1):
+    d = ((2 * h0 + h1) * m0 - h0 * m1) / (h0 + h1)
+    flip = np.sign(d) != np.sign(m0)
+    big = (np.sign(m0) != np.sign(m1)) & (np.abs(d) > 3 * np.abs(m0))
+    d = np.where(flip, 0.0, d)
+    return np.where((~flip) & big, 3 * m0, d)
+
+
+def pchip_slopes(x, y):
+    """Knot derivatives for rows of ``y`` (shape [rows, K]) at knots ``x``."""
+    x = np.asarray(x, dtype=float)
+    y = np.asarray(y, dtype=float)
+    h = np.diff(x)
+    m = np.diff(y, axis=1) / h
+    K = x.size
+    if K == 2:
+        return np.repeat(m, 2, axis=1)
+    d = np.zeros_like(y)
+    sm = np.sign(m)
+    flat = (sm[:, 1:] != sm[:, :-1]) | (m[:, 1:] == 0) | (m[:, :-1] == 0)
+    w1 = 2 * h[1:] + h[:-1]
+    w2 = h[1:] + 2 * h[:-1]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        whmean = (w1 / m[:, :-1] + w2 / m[:, 1:]) / (w1 + w2)
+        inner = 1.0 / whmean
+    d[:, 1:-1] = np.where(flat, 0.0, inner)
+    d[:, 0] = _edge_slope(h[0], h[1], m[:, 0], m[:, 1])
+    d[:, -1] = _edge_slope(h[-1], h[-2], m[:, -1], m[:, -2])
+    return d
+
+
+def pchip_coefficients(x, y):
+    """Piecewise-cubic coefficients c[4, K-1, rows] in (t - x_i) powers 3..0."""
+    x = np.asarray(x, dtype=float)
+    y = np.asarray(y, dtype=float)
+    d = pchip_slopes(x, y)
+    h = np.diff(x)
+    m = np.diff(y, axis=1) / h
+    t = (d[:, :-1] + d[:, 1:] - 2 * m) / h
+    c = np.empty((4, x.size - 1, y.shape[0]))
+    c[0] = (t / h).T
+    c[1] = ((m - d[:, :-1]) / h - t).T
+    c[2] = d[:, :-1].T
+    c[3] = y[:, :-1].T
+    return c
+
+
+def ppoly_eval(x, c, ph):
+    """Evaluate the piecewise cubic at phases ``ph`` (extrapolating with the end
+    pieces); returns [rows, len(ph)]."""
+    ph = np.asarray(ph, dtype=float)
+    i = np.clip(np.searchsorted(x, ph, side="right") - 1, 0, x.size - 2)
+    t = ph - x[i]
+    out = c[0, i] * t[:, None]
+    out = (out + c[1, i]) * t[:, None]
+    out = (out + c[2, i]) * t[:, None]
+    out = out + c[3, i]
+    return out.T
+
+
+# ---------------------------------------------------------------------------
+# portraits
+# ---------------------------------------------------------------------------
+class PulsePortrait(object):
+    """portraits.py:9-91."""
+    _profiles = None
+
+    def __call__(self, phases=None):
+        if phases is None:
+            if self._profiles is None:
+                print("Warning: base profiles not generated, returning `None`")
+            return self._profiles
+        return self.calc_profiles(phases)
+
+    def init_profiles(self, Nphase, Nchan=None):
+        """portraits.py:32-45: sample at arange(N)/N, renormalise to max 1."""
+        ph = np.arange(Nphase) / Nphase
+        self._profiles = self.calc_profiles(ph, Nchan=Nchan)
+        self._Amax = self._profiles.max()
+        self._profiles = self._profiles / self.Amax
+        self._max_profile = [pr for pr in self._profiles if pr.max() == 1.0][0]
+
+    def calc_profiles(self, phases, Nchan=None):
+        raise NotImplementedError()
+
+    def _calcOffpulseWindow(self, Nphase=None):
+        """portraits.py:62-82: argmin over a sliding trapezoid of width Nph/8
+        (circular), window returned as float indices mod Nph."""
+        ws = (2048 / 8) if Nphase is None else Nphase / 8
+        half = ws // 2
+        prof = np.asarray(self._max_profile, dtype=float)
+        n = len(prof)
+        integral = np.zeros_like(prof)
+        lo = int(-half)
+        width = int(2 * half)
+        # trapezoid over `width` consecutive (circular) samples starting at i-half
+        idx = (np.arange(n)[:, None] + lo + np.arange(width)[None, :]) % Nphase
+        w = prof[idx]
+        integral[:] = w.sum(axis=1) - 0.5 * (w[:, 0] + w[:, -1]) if width > 1 else 0.0
+        minind = np.argmin(integral)
+        return np.arange(minind - half, minind + half + 1) % Nphase
+
+    @property
+    def profiles(self):
+        return self._profiles
+
+    @property
+    def Amax(self):
+        return self._Amax
+
+
+def _gauss_single(ph, peak, width, amp):
+    if np.any(ph > 1) or np.any(ph < 0):
+        raise ValueError('Phase values must all lie within [0,1].')
+    return amp * np.exp(-0.5 * ((ph - peak) / width) ** 2)
+
+
+def _gauss_sum(ph, peaks, widths, amps):
+    if np.any(ph > 1) or np.any(ph < 0):
+        raise ValueError('Phase values must all lie within [0,1].')
+    return np.sum(amps[:, None] * np.exp(-0.5 * ((ph[None, :] - peaks[:, None]) / widths[:, None]) ** 2),
+                  axis=0)
+
+
+class GaussPortrait(PulsePortrait):
+    """portraits.py:94-198: sum of Gaussian components; 1-D parameters are
+    tiled over channels, 2-D parameters give one row per channel."""
+
+    def __init__(self, peak=0.5, width=0.05, amp=1):
+        self._peak = peak
+        self._width = width
+        self._amp = amp
+        self._profiles = None
+
+    def init_profiles(self, Nphase, Nchan=None):
+        """portraits.py:131-140 (no renormalisation)."""
+        ph = np.arange(Nphase) / Nphase
+        self._profiles = self.calc_profiles(ph, Nchan=Nchan)
+        self._max_profile = [pr for pr in self._profiles if pr.max() == 1.0][0]
+
+    def calc_profiles(self, phases, Nchan=None):
+        ph = np.array(phases)
+        if hasattr(self.peak, 'ndim') and self.peak.ndim == 2:
+            profiles = np.array([_gauss_sum(ph, self.peak[:], self.width[:], self.amp[:])
+                                 for _ in range(self.peak.shape[0])])
+        else:
+            if Nchan is None:
+                raise ValueError('Nchan must be provided if only 1-dim profile information provided.')
+            if hasattr(self.peak, 'ndim') and self.peak.ndim == 1:
+                one = _gauss_sum(ph, self.peak, self.width, self.amp)
+            else:
+                one = _gauss_single(ph, self.peak, self.width, self.amp)
+            profiles = np.tile(one, (Nchan, 1))
+        self._Amax = self.Amax if hasattr(self, '_Amax') else np.amax(profiles)
+        return profiles / self._Amax
+
+    @property
+    def peak(self):
+        return self._peak
+
+    @property
+    def width(self):
+        return self._width
+
+    @property
+    def amp(self):
+        return self._amp
+
+    @property
+    def Amax(self):
+        return self._Amax
+
+
+class DataPortrait(PulsePortrait):
+    """portraits.py:200-267: PCHIP through the sampled profiles; periodicity is
+    enforced by appending the first column (phases arange(N+1)/N) when the
+    first and last columns differ."""
+
+    def __init__(self, profiles, phases=None):
+        profiles = np.asarray(profiles)
+        if np.any(profiles < 0.0):
+            log.warning("Some phase bins of input profile are negative, replacing them with zeros...")
+            for prof in profiles:
+                if np.any(prof < 0.0):
+                    prof[np.where(prof < 0.0)[0]] = 0.0
+        if phases is None:
+            N = profiles.shape[1]
+            if any(a != b for a, b in zip(profiles[:, 0], profiles[:, -1])):
+                profiles = np.append(profiles, profiles[:, 0][:, np.newaxis], axis=1)
+                phases = np.arange(N + 1) / N
+            else:
+                phases = np.arange(N) / N
+        else:
+            phases = np.asarray(phases, dtype=float)
+            if phases[-1] != 1:
+                phases = np.append(phases, 1)
+                profiles = np.append(profiles, profiles[:, 0][:, np.newaxis], axis=1)
+            elif any(a != b for a, b in zip(profiles[:, 0], profiles[:, -1])):
+                profiles[:, -1] = profiles[:, 0]
+        self._knots = np.asarray(phases, dtype=float)
+        self._kvals = np.asarray(profiles, dtype=float)
+        self._coef = pchip_coefficients(self._knots, self._kvals)
+
+    def _generator(self, phases):
+        return ppoly_eval(self._knots, self._coef, phases)
+
+    def calc_profiles(self, phases, Nchan=None):
+        profiles = self._generator(phases)
+        Amax = self.Amax if hasattr(self, '_Amax') else np.max(profiles)
+        return profiles / Amax
+
+    # -- device export --------------------------------------------------
+    def uniform_knots(self):
+        """(M, nint) when the knots are k/M (k = 0..nint), else None."""
+        x = self._knots
+        nint = x.size - 1
+        M = int(round(1.0 / (x[1] - x[0]))) if nint >= 1 else 0
+        if M < 1 or not np.allclose(x, np.arange(x.size) / M, rtol=0, atol=1e-15):
+            return None
+        return M, nint
+
+    def device_table(self):
+        """float32 [rows, nint, 4] coefficients in the local coordinate
+        u = (phase - k/M) * M, ordered (u^3, u^2, u^1, u^0), divided by Amax
+        so the device evaluates calc_profiles directly; plus (M, nint)."""
+        geo = self.uniform_knots()
+        if geo is None:
+            raise NotImplementedError("non-uniform portrait phases on the device path")
+        M, nint = geo
+        h = 1.0 / M
+        amax = self.Amax if hasattr(self, '_Amax') else 1.0
+        c = self._coef  # [4, nint, rows]
+        tab = np.stack([c[0] * h ** 3, c[1] * h ** 2, c[2] * h, c[3]], axis=-1)  # [nint, rows, 4]
+        tab = np.transpose(tab, (1, 0, 2)) / amax
+        return np.ascontiguousarray(tab, dtype=np.float32), M, nint
+
+
+class UserPortrait(PulsePortrait):
+    """portraits.py:270-275."""
+
+    def __init__(self):
+        raise NotImplementedError()

@@ -1,0 +1,205 @@
+"""Pulsar -- mirrors ``psrsigsim/pulsar/pulsar.py``.
+
+make_pulses builds the host plan (Nph, nsamp, nsub, Nfold, draw_norm, the
+spectral-index-scaled PCHIP portrait) exactly as the reference does
+(pulsar.py:86-151) and records a *source* stage; the (Nchan, nsamp)
+intensities -- profile x chi2 draws x draw_norm -- are generated on the GPU
+inside the fused run.  null() derives shift_val / the pulse choice / the
+off-pulse level on the host and records a null stage (pulsar.py:246-333).
+"""
+import math
+
+import numpy as np
+
+from .profiles import GaussProfile, DataPortrait
+from .._units import make_quant, Quantity, to_value
+from .. import _engine
+
+__all__ = ["Pulsar"]
+
+
+class Pulsar(object):
+    """pulsar.py:11-84."""
+
+    def __init__(self, period, Smean, profiles=None, name=None, specidx=0.0, ref_freq=None):
+        self._period = make_quant(period, 's')
+        self._Smean = make_quant(Smean, 'Jy')
+        self._name = name
+        self._specidx = specidx
+        if ref_freq is not None:
+            self._ref_freq = make_quant(ref_freq, "MHz")
+        else:
+            self._ref_freq = ref_freq
+        self._Profiles = GaussProfile() if profiles is None else profiles
+
+    def __repr__(self):
+        namestr = "" if self.name is None else self.name + ", "
+        return "Pulsar(" + namestr + "{})".format(self.period.to('ms'))
+
+    @property
+    def Profiles(self):
+        return self._Profiles
+
+    @property
+    def name(self):
+        return self._name
+
+    @property
+    def period(self):
+        return self._period
+
+    @property
+    def Smean(self):
+        return self._Smean
+
+    @property
+    def specidx(self):
+        return self._specidx
+
+    @property
+    def ref_freq(self):
+        return self._ref_freq
+
+    # -- helpers -------------------------------------------------------------
+    def _P(self):
+        return float(to_value(self._period, 's'))
+
+    def _nph(self, signal):
+        """int((samprate * period).decompose()) (pulsar.py:96, 124)."""
+        return int((signal._samprate_MHz() * self._P()) * 1e6)
+
+    def _add_spec_idx(self, signal):
+        """pulsar.py:86-105: resample the profile to Nph phases, scale by
+        (f/ref)^specidx, wrap it as a DataPortrait (PCHIP)."""
+        C = (np.asarray(signal._freqs_MHz()) / float(to_value(self.ref_freq, 'MHz'))) ** self.specidx
+        C = np.reshape(C, (signal.Nchan, 1))
+        Nph = self._nph(signal)
+        self.Profiles.init_profiles(Nph, Nchan=signal.Nchan)
+        full_profs = self.Profiles.calc_profiles(np.linspace(0.0, 1.0, Nph), Nchan=signal.Nchan)
+        full_profs *= C   # in place: a 1-row portrait with Nchan > 1 raises, as there
+        self._Profiles = DataPortrait(full_profs)
+
+    def make_pulses(self, signal, tobs):
+        """pulsar.py:107-151 (filterbank signals)."""
+        signal._tobs = make_quant(tobs, 's')
+        if self.ref_freq is None:
+            self._ref_freq = signal.fcent
+        if signal.sigtype != "FilterBankSignal":
+            raise NotImplementedError("no pulse method for signal: {}".format(signal.sigtype))
+        self._add_spec_idx(signal)
+        Nph = self._nph(signal)
+        self.Profiles.init_profiles(Nph, signal.Nchan)
+        self._make_pow_pulses(signal)
+        pr = self.Profiles._max_profile
+        signal._Smax = self.Smean * len(pr) / np.sum(pr)
+
+    def _make_amp_pulses(self, signal):
+        raise NotImplementedError("amplitude (baseband/RF) pulses are outside the filterbank path")
+
+    def _make_pow_pulses(self, signal):
+        """pulsar.py:185-244: fold -> tile(profiles, nsub) x chi2(Nfold);
+        search -> PCHIP(phase(n)) x chi2(1).  Recorded as the source stage."""
+        P = self._P()
+        sr = signal._samprate_MHz()
+        tobs = float(to_value(signal.tobs, 's'))
+        call = _engine.next_call()
+        inj = _engine.take_injection("gen")
+        if signal.fold:
+            if signal.sublen is None:
+                signal._sublen = signal.tobs
+                signal._nsub = 1
+            else:
+                signal._nsub = int(np.round(tobs / float(to_value(signal.sublen, 's'))))
+            signal._nsamp = int((signal._nsub * (P * sr)) * 1e6)
+            table = np.asarray(self.Profiles(), dtype=np.float64)
+            Nph = table.shape[1]
+            nfold = float(to_value(signal.sublen, 's')) / P
+            signal._Nfold = Quantity(nfold, '')
+            signal._set_draw_norm(df=nfold)
+            ncols = Nph * signal._nsub
+            src = _engine.Source("fold", _dedupe(table).astype(np.float32), nfold,
+                                 signal._draw_norm, call, nph=Nph, inj=inj)
+        else:
+            signal._sublen = self.period
+            signal._nsub = int(np.round(tobs / P))
+            signal._set_draw_norm(df=1)
+            signal._nsamp = int((tobs * sr) * 1e6)
+            ncols = signal._nsamp
+            tab, M, nint = self.Profiles.device_table()
+            tab = _dedupe(tab)
+            spp = (sr * P) * 1e6                      # samples per period
+            inv = 1.0 / spp                           # cycles per sample
+            step = int(round(math.ldexp(inv - math.floor(inv), 64)))
+            src = _engine.Source("search", tab, 1.0, signal._draw_norm, call, M=M, nint=nint,
+                                 phase_step=step % (1 << 64), inj=inj)
+        signal._ncols = int(ncols)
+        signal._pending = _engine.Pending(src)
+        signal._row0 = None
+
+    def null(self, signal, null_frac, length=None, frequency=None):
+        """pulsar.py:246-333."""
+        null_pulses = int(np.round(signal.nsub * null_frac))
+        Nph = self._nph(signal)
+        opw = self.Profiles._calcOffpulseWindow(Nphase=Nph)
+        if signal.fold:
+            df = float(signal.Nfold)
+        else:
+            df = 1.0
+        if not signal.fold or float(signal.Nfold) < 100:
+            check_df = 100.0
+        else:
+            check_df = float(signal.Nfold)
+        pend = signal._pending if signal._pending is not None else _engine.Pending(None)
+        if pend.null is not None or pend.noise is not None:
+            signal._flush()
+            pend = _engine.Pending(None)
+        row0 = _engine.probe_row0(signal, pend, Nph)
+        where = np.where(row0 == np.max(row0))[0]
+        shift_val = Nph // 2 - where
+        if length is not None or frequency is not None:
+            raise NotImplementedError("Length and Frequency not been implimented yet")
+        if shift_val.size != 1:
+            raise ValueError("operands could not be broadcast together with shapes (%d,) (%d,)"
+                             % (Nph, shift_val.size))
+        shift_val = int(shift_val[0])
+        call = _engine.next_call()
+        rand_pulses = _engine.take_injection("null_pulses")
+        if rand_pulses is None:
+            rand_pulses = _engine.host_rng(call).choice(signal.nsub, null_pulses, replace=False)
+        rand_pulses = np.asarray(rand_pulses, dtype=np.int64)
+        rank = np.full(max(int(signal.nsub), 1), -1, dtype=np.int32)
+        for r, p in enumerate(rand_pulses):
+            rank[p] = r
+        opm = float(np.mean(self.Profiles._max_profile[opw.astype(int)]))
+        dn = float(signal._draw_norm)
+        st = {"rank": rank, "shift_val": shift_val, "nph": Nph, "call_id": call,
+              "inj_box": _engine.take_injection("box"), "inj_rep": _engine.take_injection("rep")}
+        if null_pulses == 0 or rand_pulses.size == 0:
+            return
+        if signal.delay is None:
+            st.update(mode="undelayed", box_df=df, box_scale=dn * opm)
+            if signal._pending is None:
+                signal._pending = _engine.Pending(None)
+            signal._pending.null = st
+            return
+        total_ms = np.asarray(to_value(signal.delay, 'ms'), dtype=np.float64)
+        mask_samples = total_ms / signal._dt_ms()
+        st.update(mode="delayed", box_df=check_df, box_scale=dn, rep_df=df, rep_scale=dn * opm,
+                  mask_samples=mask_samples)
+        pend = signal._pending
+        if pend is not None and pend.shifts:
+            fused = np.sum(pend.shifts, axis=0)
+            if np.allclose(fused, mask_samples, rtol=1e-12, atol=1e-9):
+                pend.null = st
+                return
+        # the data already carries (part of) the delay: shift only the mask
+        signal._flush()
+        signal._pending = _engine.Pending(None)
+        signal._pending.null = st
+
+
+def _dedupe(tab):
+    """One shared row when every channel's table is identical."""
+    if tab.shape[0] > 1 and np.all(tab == tab[0:1]):
+        return np.ascontiguousarray(tab[0:1])
+    return np.ascontiguousarray(tab)

@@ -1,0 +1,2 @@
+from .signal import Signal, BaseSignal  # noqa: F401
+from .fb_signal import FilterBankSignal  # noqa: F401

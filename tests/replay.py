@@ -1,0 +1,204 @@
+"""Replay the golden cases (tests/golden/make_golden.py) through
+psrsigsim_amd on the GPU with the reference's own recorded draws injected,
+and compare every stage with the reference outputs stored in the fixtures.
+
+A case is a small script of API calls; the same script is interpreted by the
+CPU oracle (to derive the injected box / replacement rows and the null
+bookkeeping) and by the product.  ``fused=True`` reads the data only at the
+end (every stage runs inside one fused device run where possible);
+``fused=False`` reads ``signal.data`` after every call (each stage flushed on
+its own).  Returns {stage: normwise error} with the error defined per channel
+as max|gpu - ref| / max|ref| (SURVEY.md §8(d) parity gate, 1e-5).
+"""
+import os
+
+import numpy as np
+
+from oracle import pss_cpu as O
+from tests.fixtures_util import load
+
+FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fixtures")
+
+
+def _prof():
+    return np.load(os.path.join(FIX, "j1713_search.npz"))["input_profile"]
+
+
+CASES = {
+    "tutorial1": dict(
+        sig=dict(fcent=1400, bw=400, nchan=2), psr=dict(period=0.005, Smean=10, prof=("gauss", 0.5, 0.05, 1)),
+        ops=[("make_pulses", 1.0, "pulses"), ("disperse", 10, "disperse"),
+             ("observe", "Arecibo", "Lband_PUPPI", True, "noise")]),
+    "northstar_mini": dict(
+        sig=dict(fcent=1400, bw=400, nchan=4, fold=False), psr=dict(period=0.005, Smean=1.0, prof=("gauss", 0.5, 0.05, 1)),
+        ops=[("scatter_conv", 1e-4, 1400, None), ("make_pulses", 8192 * 20.48e-6, "pulses"),
+             ("disperse", 100, "disperse"), ("fd", [2e-4, -3e-5], "fd"),
+             ("scatter_shift", 3e-4, 1400, "scatter"), ("null", 0.1, "null"),
+             ("observe", "Arecibo", "Lband_PUPPI", True, "noise")]),
+    "j1713_search": dict(
+        sig=dict(fcent=1500, bw=800, nchan=4, samprate=0.048828125, fold=False),
+        psr=dict(period=1.0 / 218.8118437960826270, Smean=0.009, prof=("data", 4)),
+        ops=[("make_pulses", 4096 * 20.48e-6, "pulses"), ("disperse", 15.917131, "disperse"),
+             ("observe", "GBT", "Lband_GUPPI", True, "noise")]),
+    "fold_sublen": dict(
+        sig=dict(fcent=1400, bw=400, nchan=2, samprate=1.0 * 2048 * 10 ** -6, sublen=0.5),
+        psr=dict(period=1.0, Smean=1.0, prof=("data", 2)),
+        ops=[("make_pulses", 2.0, "pulses"), ("disperse", 10.0, "disperse"), ("null", 0.34, "null"),
+             ("observe", "GBT", "Lband_GUPPI", True, "noise")]),
+    "null_undelayed": dict(
+        sig=dict(fcent=1400, bw=400, nchan=3, fold=False), psr=dict(period=0.005, Smean=2.0, prof=("gauss", 0.45, 0.03, 1)),
+        ops=[("make_pulses", 4096 * 20.48e-6, "pulses"), ("null", 0.3, "null"), ("disperse", 5, "disperse"),
+             ("observe", "Arecibo", "Lband_PUPPI", False, None)]),
+    "specidx_int8": dict(
+        sig=dict(fcent=1400, bw=400, nchan=4, dtype=np.int8),
+        psr=dict(period=0.005, Smean=1.0, prof=("gaussarr",), specidx=-1.6, ref_freq=1300),
+        ops=[("make_pulses", 1.0, "pulses"), ("disperse", 20, "disperse"),
+             ("observe", "Arecibo", "Lband_PUPPI", True, "noise")]),
+}
+for _tag, _dt in (("eq", 4.8828125e-06), ("down", 9.765625e-06), ("rebin", 7.5e-06)):
+    CASES["observe_" + _tag] = dict(
+        sig=dict(fcent=1400, bw=400, nchan=2, fold=False, samprate=(1.0 / 0.005) * 2048 * 10 ** -6),
+        psr=dict(period=0.005, Smean=10, prof=("gauss", 0.5, 0.05, 1)),
+        ops=[("make_pulses", 0.02, "pulses"), ("observe", ("custom", _dt), "T", True, "noise")])
+
+
+# ---------------------------------------------------------------------------
+# oracle interpretation (derives the injections)
+# ---------------------------------------------------------------------------
+def _oracle_profile(spec):
+    kind = spec[0]
+    if kind == "gauss":
+        return O.GaussPortrait(*spec[1:])
+    if kind == "gaussarr":
+        return O.GaussPortrait(np.array([0.3, 0.6]), np.array([0.02, 0.05]), np.array([0.5, 1.0]))
+    return O.DataProfile(_prof(), nchan=spec[1])
+
+
+def oracle_run(name):
+    meta, A, draws = load(name)
+    case = CASES[name]
+    d = O.InjectedDraws(draws)
+    sg = case["sig"]
+    sig = O.Signal(sg["fcent"], sg["bw"], nchan=sg["nchan"], samprate=sg.get("samprate"),
+                   sublen=sg.get("sublen"), dtype=sg.get("dtype", np.float32), fold=sg.get("fold", True))
+    ps = case["psr"]
+    psr = O.Pulsar(ps["period"], ps["Smean"], profiles=_oracle_profile(ps["prof"]),
+                   specidx=ps.get("specidx", 0.0), ref_freq=ps.get("ref_freq"))
+    inj = {}
+    for op in case["ops"]:
+        k = op[0]
+        if k == "make_pulses":
+            i0 = d.i
+            O.make_pulses(sig, psr, op[1], d)
+            inj["gen"] = draws[i0][2]
+        elif k == "disperse":
+            O.disperse(sig, op[1])
+        elif k == "fd":
+            O.FD_shift(sig, op[1])
+        elif k == "scatter_shift":
+            O.scatter_broaden(sig, op[1], op[2], convolve=False)
+        elif k == "scatter_conv":
+            O.scatter_broaden(sig, op[1], op[2], convolve=True, pulsar=psr)
+        elif k == "null":
+            info = O.null(sig, psr, op[1], d)
+            inj["null_pulses"] = info["pulses"]
+            inj["box"] = info["box_row"]
+            inj["rep"] = info["rep_dense"]
+            inj["shift_val"] = int(np.asarray(info["shift_val"])[0])
+        elif k == "observe":
+            if op[3]:
+                inj["noise"] = draws[len(draws) - 1][2]
+    return meta, A, inj
+
+
+# ---------------------------------------------------------------------------
+# product interpretation
+# ---------------------------------------------------------------------------
+def _err(gpu, ref):
+    gpu = np.asarray(gpu, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    if gpu.shape != ref.shape:
+        return float("inf")
+    ref2 = ref.reshape(ref.shape[0], -1) if ref.ndim > 1 else ref[None]
+    gpu2 = gpu.reshape(ref2.shape)
+    scale = np.maximum(np.max(np.abs(ref2), axis=1), 1e-30)
+    return float(np.max(np.max(np.abs(gpu2 - ref2), axis=1) / scale))
+
+
+def run_case(name, fused=True):
+    import psrsigsim_amd as pss
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, GaussProfile, DataProfile
+    from psrsigsim_amd.ism import ISM
+    from psrsigsim_amd.telescope import telescope as T
+    from psrsigsim_amd.telescope import Telescope, Receiver, Backend
+    from psrsigsim_amd._units import Quantity
+
+    meta, A, inj = oracle_run(name)
+    case = CASES[name]
+    sg = case["sig"]
+    sig = FilterBankSignal(sg["fcent"], sg["bw"], Nsubband=sg["nchan"], sample_rate=sg.get("samprate"),
+                           sublen=sg.get("sublen"), dtype=sg.get("dtype", np.float32),
+                           fold=sg.get("fold", True))
+    ps = case["psr"]
+    spec = ps["prof"]
+    if spec[0] == "gauss":
+        prof = GaussProfile(*spec[1:])
+    elif spec[0] == "gaussarr":
+        prof = GaussProfile(np.array([0.3, 0.6]), np.array([0.02, 0.05]), np.array([0.5, 1.0]))
+    else:
+        prof = DataProfile(_prof(), Nchan=spec[1])
+    psr = Pulsar(ps["period"], ps["Smean"], profiles=prof, specidx=ps.get("specidx", 0.0),
+                 ref_freq=ps.get("ref_freq"))
+    ism = ISM()
+    errs = {}
+    pss.seed(1)
+
+    def snap(tag):
+        if tag is not None and not fused:
+            errs[tag] = _err(sig.data.cpu().numpy(), A["data_" + tag])
+
+    for op in case["ops"]:
+        k = op[0]
+        if k == "make_pulses":
+            pss.inject(gen=inj["gen"])
+            psr.make_pulses(sig, op[1])
+            snap(op[2])
+        elif k == "disperse":
+            ism.disperse(sig, op[1])
+            snap(op[2])
+        elif k == "fd":
+            ism.FD_shift(sig, op[1])
+            snap(op[2])
+        elif k == "scatter_shift":
+            ism.scatter_broaden(sig, op[1], op[2], convolve=False)
+            snap(op[3])
+        elif k == "scatter_conv":
+            ism.scatter_broaden(sig, op[1], op[2], convolve=True, pulsar=psr)
+        elif k == "null":
+            pss.inject(null_pulses=inj["null_pulses"], box=inj["box"])
+            if inj["rep"] is not None:
+                pss.inject(rep=inj["rep"])
+            psr.null(sig, op[1])
+            snap(op[2])
+        elif k == "observe":
+            tel_spec, system, noise, tag = op[1], op[2], op[3], op[4]
+            if tel_spec == "Arecibo":
+                tel = T.Arecibo()
+            elif tel_spec == "GBT":
+                tel = T.GBT()
+            else:
+                tel = Telescope(20.0, area=None, Tsys=25.0, name="Twenty_Meter")
+                tel.add_system(name="T", receiver=Receiver(fcent=1400, bandwidth=400, name="Lband"),
+                               backend=Backend(samprate=1.0 / Quantity(tel_spec[1], "s"), name="Cyborg"))
+            if noise:
+                pss.inject(noise=inj["noise"])
+            out = tel.observe(sig, psr, system=system, noise=noise, ret_resampsig=True)
+            errs["out"] = _err(out.cpu().numpy().astype(np.float64), A["out"])
+            if tag is not None:
+                errs[tag] = _err(sig.data.cpu().numpy(), A["data_" + tag])
+    # the final state is always compared
+    last = [op for op in case["ops"] if op[-1] is not None and op[0] != "observe"]
+    if fused and case["ops"][-1][0] != "observe" and last:
+        errs[last[-1][-1]] = _err(sig.data.cpu().numpy(), A["data_" + last[-1][-1]])
+    return errs

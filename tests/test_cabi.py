@@ -1,0 +1,62 @@
+"""CPU-side checks of the C ABI: the library loads, exports every function
+include/pss_hip.h declares, and ctypes' PssPipeline has exactly the C layout
+(offsets compared against a gcc build of the header)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from psrsigsim_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "pss_hip.h")
+
+
+def header_functions():
+    txt = open(HDR).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(pss_\w+)\s*\(", txt)))
+
+
+def test_library_loads_and_exports_everything():
+    L = _lib.load()
+    names = header_functions()
+    assert "pss_run" in names and len(names) >= 9
+    for n in names:
+        assert hasattr(L, n), n
+        assert n in _lib.EXPORTS, n
+    assert L.pss_version() >= 100
+
+
+def test_workspace_sizes():
+    L = _lib.load()
+    assert L.pss_workspace_bytes(4, 4096) == 0            # single pass, LDS only
+    assert L.pss_workspace_bytes(4, 1 << 20) == 4 * (1 << 20) * 8
+    assert L.pss_workspace_bytes(2, 244) == 2 * 2 * 244 * 8 + 244 * 8   # fallback
+
+
+def test_struct_layout_matches_header(tmp_path):
+    fields = [f for f, _ in _lib.PssPipeline._fields_]
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "pss_hip.h"', 'int main(void){',
+           'printf("%zu\\n", sizeof(PssPipeline));']
+    src += ['printf("%%zu\\n", offsetof(PssPipeline, %s));' % f for f in fields]
+    src += ['return 0;}']
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I" + os.path.join(ROOT, "include"), str(c), "-o", str(exe)], check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert vals[0] == ctypes.sizeof(_lib.PssPipeline)
+    for f, off in zip(fields, vals[1:]):
+        assert getattr(_lib.PssPipeline, f).offset == off, f
+
+
+def test_error_mapping():
+    with pytest.raises(ValueError):
+        _lib.check(_lib.PSS_EINVAL)
+    with pytest.raises(NotImplementedError):
+        _lib.check(_lib.PSS_EUNSUPPORTED)
+    with pytest.raises(RuntimeError):
+        _lib.check(_lib.PSS_EHIP)
