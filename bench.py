@@ -1,0 +1,207 @@
+#!/usr/bin/env python
+"""Benchmark of the filterbank synthesis path (BASELINE.json metric).
+
+One *step* = one pass of the north-star pipeline (config C3) over a freshly
+made signal, through the drop-in API exactly as Simulation.simulate strings it
+(simulate/simulate.py:292-326) plus the C3 null:
+
+    FilterBankSignal(1400, 400, Nsubband=2048, fold=False)       (20.48 us)
+    ISM.scatter_broaden(tau_d=1e-4 s, 1400 MHz, convolve=True)   (profile level)
+    Pulsar(5 ms, GaussProfile(0.5, 0.05, 1)).make_pulses(tobs = 2^22 * 20.48 us)
+    ISM.disperse(DM=100)
+    Pulsar.null(0.1)                       (delayed branch: mask through the FFT)
+    Arecibo().observe('Lband_PUPPI', noise=True)
+
+= 2048 x 2^22 channel-samples per GPU, synthetic (Philox) data, fp32 compute.
+Host planning, the channel-0 probe for null's shift_val and the fused device
+run are all inside the timed region.  With --gpus N (torch.distributed, one
+rank per GPU) each rank owns its own 2048-channel block of a 2048*N-channel
+signal (weak scaling; no collective on the data path; shard-invariant RNG).
+
+Reports (one JSON line on rank 0): value = channel-samples/s over all ranks,
+the roofline of the dominant kernel (HIP events on the launch stream, inside
+the timed region), and the CPU oracle timed on a bounded channel sample.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "channel-samples/sec (node) at 2048ch x 2^22 samp; % HBM roofline; speedup vs CPU"
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md chip table (spec)
+NCHAN = 2048
+LOG2N = 22
+TOBS_PER_SAMPLE = 20.48e-6
+
+# algorithmic HBM bytes per channel-sample of each kernel in the C3 run
+# (complex64 spill = 8 B, real fp32 in/out = 4 B; DESIGN.md "Roofline")
+ALG_BYTES = {"fourstep_colA": 8.0, "fourstep_row": 16.0, "fourstep_colC": 12.0,
+             "single_pass": 4.0, "elementwise": 4.0, "fallback_dft": 28.0}
+
+
+def c3_step(pss, nchan_total, shard, nsamp_log2, ret_out=False):
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+    from psrsigsim_amd.ism import ISM
+    from psrsigsim_amd.telescope import telescope as T
+    sig = FilterBankSignal(1400, 400, Nsubband=nchan_total, fold=False, shard=shard)
+    psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
+    ism = ISM()
+    ism.scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
+    psr.make_pulses(sig, tobs=(1 << nsamp_log2) * TOBS_PER_SAMPLE)
+    ism.disperse(sig, 100)
+    psr.null(sig, 0.1)
+    T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True, ret_resampsig=ret_out)
+    return sig
+
+
+def cpu_baseline(nch, nsamp_log2):
+    """The oracle (NumPy restatement with the reference's call structure:
+    per-channel rfft/irfft, legacy RandomState chi2, scipy PCHIP), single
+    process, on `nch` channels of the same pipeline."""
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    from oracle import pss_cpu as O
+    d = O.LegacyDraws(1776)
+    t0 = time.perf_counter()
+    sig = O.Signal(1400, 400, nchan=nch, fold=False)
+    psr = O.Pulsar(0.005, 1.0, profiles=O.GaussPortrait(0.5, 0.05, 1))
+    O.scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
+    O.make_pulses(sig, psr, (1 << nsamp_log2) * TOBS_PER_SAMPLE, d)
+    O.disperse(sig, 100)
+    O.null(sig, psr, 0.1, d)
+    O.observe(sig, psr, O.Arecibo(), "Lband_PUPPI", d, noise=True)
+    dt = time.perf_counter() - t0
+    return nch * (1 << nsamp_log2) / dt, dt
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nchan", type=int, default=NCHAN, help="channels per GPU")
+    ap.add_argument("--log2n", type=int, default=LOG2N)
+    ap.add_argument("--cpu-chans", type=int, default=8, help="oracle sample size (channels)")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import psrsigsim_amd as pss
+    from psrsigsim_amd import _lib
+    _lib.lib()
+    pss.seed(1776)
+
+    C = args.nchan
+    total = C * world
+    shard = (rank * C, (rank + 1) * C)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        s = c3_step(pss, total, shard, args.log2n)
+        del s
+    barrier()
+    _lib.load().pss_timing_enable(1)
+    _lib.timing_collect()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        s = c3_step(pss, total, shard, args.log2n)
+        del s
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    _lib.load().pss_timing_enable(0)
+    launches = _lib.timing_collect()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    per_step = elapsed / args.steps
+    units = float(total) * (1 << args.log2n)
+    value = units / per_step
+
+    # dominant kernel of the full-size launches
+    full = C * (1 << args.log2n)
+    agg = {}
+    for kind, ms, u in launches:
+        if u != full:
+            continue
+        a = agg.setdefault(kind, [0.0, 0])
+        a[0] += ms
+        a[1] += 1
+    gpu_ms = sum(v[0] for v in agg.values()) / max(args.steps, 1)
+    dom = max(agg, key=lambda k: agg[k][0]) if agg else None
+    roof = None
+    kernels = {}
+    for k, (ms, n) in agg.items():
+        avg = ms / n
+        b = ALG_BYTES.get(k, 0.0) * full
+        kernels[k] = {"avg_ms": round(avg, 4), "launches": n, "alg_bytes": b,
+                      "GBps": round(b / (avg * 1e-3) / 1e9, 1)}
+    if dom is not None:
+        avg_ms = agg[dom][0] / agg[dom][1]
+        bytes_launch = ALG_BYTES[dom] * full
+        ach = bytes_launch / (avg_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
+                "avg_launch_ms": round(avg_ms, 4), "alg_bytes_per_launch": bytes_launch}
+
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        v, dt = cpu_baseline(args.cpu_chans, args.log2n)
+        cpu = {"value": round(v, 1), "unit": "channel-samples/s", "cores": 1, "kind": "port",
+               "sample": "%d ch x 2^%d samp of the same C3 pipeline, oracle/pss_cpu.py (float64 NumPy, "
+                         "reference call structure), single process, %.1f s on %s"
+                         % (args.cpu_chans, args.log2n, dt, cpu_model())}
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "channel-samples/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(per_step * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (Philox chi2 pulses/noise)",
+            "config": {"workload": "C3 north-star: FilterBankSignal 2048 ch x 2^22 samp per GPU, GaussProfile "
+                                   "P=5 ms, scatter_broaden(1e-4 s, convolve) + disperse(DM=100) + "
+                                   "null(0.1) + Arecibo Lband_PUPPI radiometer noise",
+                       "nchan_per_gpu": C, "nsamp": 1 << args.log2n, "parallelism": "channel-shard x%d" % world},
+            "gpu_kernel_ms_per_step": round(gpu_ms, 3),
+            "kernels": kernels,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "speedup_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -139,6 +139,15 @@ typedef struct PssPipeline {
 int pss_version(void);
 int pss_last_error(char *buf, size_t n);
 
+/* Opt-in kernel timing for benchmarks: while enabled, pss_run records a pair
+ * of hipEvents on its stream around every kernel it launches.  collect()
+ * synchronises on them and returns, per launch (up to `cap`), the kernel kind
+ * (0 elementwise, 1 single pass, 2 four-step column pass A, 3 row pass B,
+ * 4 column pass C, 5 fallback), its milliseconds and the channel-samples it
+ * processed; returns the number of launches reported and resets. */
+void pss_timing_enable(int on);
+int pss_timing_collect(int32_t *kind, double *ms, int64_t *units, int cap);
+
 /* Workspace bytes the fused run needs for `nchan` rows of length `nsamp`. */
 int64_t pss_workspace_bytes(int32_t nchan, int64_t nsamp);
 

@@ -16,6 +16,8 @@ SRC_LOAD, SRC_SEARCH, SRC_FOLD = 0, 1, 2
 NULL_NONE, NULL_UNDELAYED, NULL_DELAYED = 0, 1, 2
 OUT_NONE, OUT_F32, OUT_I8 = 0, 1, 2
 P_PULSE, P_BOX, P_REP, P_NOISE, P_TEST = 1, 2, 3, 4, 5
+KERNEL_KINDS = ("elementwise", "single_pass", "fourstep_colA", "fourstep_row", "fourstep_colC",
+                "fallback_dft")
 
 c_i32, c_i64, c_u32, c_u64, c_f32, c_vp = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
                                            ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
@@ -44,6 +46,9 @@ EXPORTS = {
     "pss_version": (ctypes.c_int, []),
     "pss_last_error": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
     "pss_workspace_bytes": (c_i64, [c_i32, c_i64]),
+    "pss_timing_enable": (None, [ctypes.c_int]),
+    "pss_timing_collect": (ctypes.c_int, [ctypes.POINTER(c_i32), ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(c_i64), ctypes.c_int]),
     "pss_run": (ctypes.c_int, [ctypes.POINTER(PssPipeline), c_vp]),
     "pss_shift_rows": (ctypes.c_int, [c_vp, c_i32, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "pss_down_sample": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_vp]),
@@ -85,6 +90,15 @@ def lib():
     if not torch.cuda.is_available():
         raise HipUnavailable("psrsigsim_amd computes on an MI355X (HIP) device; none is visible")
     return L
+
+
+def timing_collect(cap=4096):
+    """[(kind_name, ms, channel_samples)] of the launches timed since enable."""
+    k = (c_i32 * cap)()
+    ms = (ctypes.c_double * cap)()
+    u = (c_i64 * cap)()
+    n = load().pss_timing_collect(k, ms, u, cap)
+    return [(KERNEL_KINDS[k[i]], ms[i], u[i]) for i in range(n)]
 
 
 def last_error():

@@ -59,10 +59,6 @@ struct Rng {
 __device__ __forceinline__ float u01(uint32_t x) {
     return fmaf((float)x, 2.3283064365386963e-10f, 1.1641532182693481e-10f);
 }
-__device__ __forceinline__ double u01d(uint32_t x, uint32_t y) {
-    uint64_t v = ((uint64_t)x << 21) ^ (uint64_t)(y >> 11);   // 53 bits
-    return ((double)(v & ((1ull << 53) - 1)) + 0.5) * 1.1102230246251565e-16;
-}
 
 // Four chi2(1) draws from one Philox block: z^2 with z Box-Muller normals,
 // -2 ln(u) cos^2(2 pi v) and -2 ln(u) sin^2(2 pi v).
@@ -76,39 +72,60 @@ __device__ __forceinline__ float4 chi2_1x4(uint4 r) {
     return make_float4(l0 * c0 * c0, l0 * s0 * s0, l1 * c1 * c1, l1 * s1 * s1);
 }
 
+// log1p(y) - y for |y| small, without cancellation (alternating series).
+__device__ __forceinline__ float log1p_minus(float y) {
+    if (fabsf(y) < 0.125f) {
+        const float y2 = y * y;
+        // -y^2/2 + y^3/3 - y^4/4 + ... (terms to y^10: error < 1e-10 for |y| < 1/8)
+        float s = -1.0f / 10;
+        s = fmaf(s, y, 1.0f / 9);
+        s = fmaf(s, y, -1.0f / 8);
+        s = fmaf(s, y, 1.0f / 7);
+        s = fmaf(s, y, -1.0f / 6);
+        s = fmaf(s, y, 1.0f / 5);
+        s = fmaf(s, y, -1.0f / 4);
+        s = fmaf(s, y, 1.0f / 3);
+        s = fmaf(s, y, -0.5f);
+        return s * y2;
+    }
+    return log1pf(y) - y;
+}
+
 // chi2(df) for general df > 0 = 2 * Gamma(df/2) via Marsaglia-Tsang (2000);
-// shape < 1 boosted by U^(1/a).  Double precision acceptance test (the
-// d(1 - v + ln v) term cancels catastrophically in fp32 at df ~ 1e4).
+// shape < 1 boosted by U^(1/a).  The acceptance test ln u < z^2/2 + d(1 - v +
+// ln v), v = (1 + c z)^3, is evaluated in the cancellation-free form
+// d (3 (log1p(y) - y) - 3 y^2 - y^3), y = c z, so fp32 is exact enough even
+// at df ~ 1e4 (where d ~ 5e3 and the bracket is O(1/d)).
 // Each attempt consumes one Philox block keyed (a, b, attempt).
-__device__ __noinline__ float chi2_general(const Rng &g, uint32_t a, uint32_t b, float df) {
+__device__ __forceinline__ float chi2_general(const Rng &g, uint32_t a, uint32_t b, float df) {
     if (df == 1.0f) {
         float4 q = chi2_1x4(g.bits(a, b, 0));
         return q.x;
     }
-    double shape = 0.5 * (double)df;
-    bool boost = shape < 1.0;
-    double aa = boost ? shape + 1.0 : shape;
-    double d = aa - 1.0 / 3.0;
-    double c = 1.0 / sqrt(9.0 * d);
-    double x = d;
+    const float shape = 0.5f * df;
+    const bool boost = shape < 1.0f;
+    const float aa = boost ? shape + 1.0f : shape;
+    const float d = aa - (1.0f / 3.0f);
+    const float c = rsqrtf(9.0f * d);
+    float x = d;
+    float ub = 0.5f;
     for (uint32_t t = 0; t < 64; ++t) {
         uint4 r = g.bits(a, b, t + 1);
-        double u1 = u01d(r.x, r.y);
-        double u2 = u01d(r.z, r.w);
-        // one normal from the first pair (Box-Muller), u from the rest
-        uint4 r2 = g.bits(a, b, 0x8000u + t);
-        double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
-        double v = 1.0 + c * z;
-        if (v <= 0.0) continue;
-        v = v * v * v;
-        double u = u01d(r2.x, r2.y);
-        if (log(u) < 0.5 * z * z + d - d * v + d * log(v)) {
+        const float l = -1.3862943611198906f * __builtin_amdgcn_logf(u01(r.x));
+        const float z = sqrtf(l) * __builtin_amdgcn_cosf((float)(r.y >> 8) * 5.9604644775390625e-08f);
+        const float y = c * z;
+        if (y <= -1.0f) continue;
+        const float lu = 0.6931471805599453f * __builtin_amdgcn_logf(u01(r.z));
+        const float rhs = 0.5f * z * z + d * (3.0f * log1p_minus(y) - y * y * (3.0f + y));
+        if (lu < rhs) {
+            const float v = (1.0f + y) * (1.0f + y) * (1.0f + y);
             x = d * v;
-            if (boost) x *= pow(u01d(r2.z, r2.w), 1.0 / shape);
+            ub = u01(r.w);
             break;
         }
     }
-    return (float)(2.0 * x);
+    if (boost) x *= __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(ub) / shape);
+    return 2.0f * x;
 }
 
 }  // namespace pss

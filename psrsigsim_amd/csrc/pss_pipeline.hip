@@ -48,6 +48,35 @@ static int fail(int code, const char *fmt, ...) {
     } while (0)
 
 // ---------------------------------------------------------------------------
+// opt-in per-kernel timing (bench.py): hipEvents recorded on the launch stream
+// around every kernel of pss_run, summed per kernel kind on collect.
+// ---------------------------------------------------------------------------
+enum { TK_ELEM = 0, TK_SINGLE, TK_COLA, TK_ROW, TK_COLC, TK_FALLBACK, TK_N };
+static bool g_timing = false;
+struct TimedLaunch { int kind; int64_t units; hipEvent_t a, b; };
+static TimedLaunch g_tl[4096];
+static int g_ntl = 0;
+static int g_tk_pending = -1;
+
+static int64_t g_tk_units = 0;   // samples processed by the launch being timed
+
+static void tk_begin(int kind, hipStream_t st) {
+    if (!g_timing || g_ntl >= 4096) { g_tk_pending = -1; return; }
+    TimedLaunch &t = g_tl[g_ntl];
+    if (hipEventCreate(&t.a) != hipSuccess || hipEventCreate(&t.b) != hipSuccess) { g_tk_pending = -1; return; }
+    t.kind = kind;
+    t.units = g_tk_units;
+    hipEventRecord(t.a, st);
+    g_tk_pending = kind;
+}
+static void tk_end(hipStream_t st) {
+    if (g_tk_pending < 0) return;
+    hipEventRecord(g_tl[g_ntl].b, st);
+    ++g_ntl;
+    g_tk_pending = -1;
+}
+
+// ---------------------------------------------------------------------------
 // kernel parameters
 // ---------------------------------------------------------------------------
 struct KP {
@@ -191,16 +220,21 @@ __device__ __forceinline__ void epilogue4(const KP &k, int r, int64_t n0, int cn
         for (int i = 0; i < 4; ++i) if (i < cnt) pre[i] = row[n0 + i];
     }
     if (p.null_mode == PSS_NULL_DELAYED) {
+        const bool any = (mask[0] > 1.0f) | (mask[1] > 1.0f) | (mask[2] > 1.0f) | (mask[3] > 1.0f);
+        if (any) {
+            float x[4];
+            if (p.inj_rep) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (i < cnt && mask[i] > 1.0f) {
-                if (p.inj_rep) {
-                    pre[i] = p.inj_rep[(int64_t)r * k.N + n0 + i];
-                } else {
-                    Rng g(p.seed, p.call_null, P_REP);
-                    pre[i] = chi2_general(g, (uint32_t)(n0 + i), c, p.null_rep_df) * p.null_rep_scale;
-                }
+                for (int i = 0; i < 4; ++i) x[i] = (i < cnt) ? p.inj_rep[(int64_t)r * k.N + n0 + i] : 0.f;
+            } else {
+                Rng g(p.seed, p.call_null, P_REP);
+                draw4(g, n0, c, p.null_rep_df, x);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) x[i] *= p.null_rep_scale;
             }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (i < cnt && mask[i] > 1.0f) pre[i] = x[i];
         }
     }
     if (p.out_kind == PSS_OUT_F32) {
@@ -236,6 +270,17 @@ __device__ __forceinline__ void epilogue4(const KP &k, int r, int64_t n0, int cn
     } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) if (i < cnt) row[n0 + i] = pre[i];
+    }
+}
+
+// Delayed null: the (pre-shift) box mask is the same for every channel, so it
+// is evaluated once per run into a row of N floats (0 outside the boxes) that
+// the source stage of every channel reads.
+__global__ __launch_bounds__(256) void k_box_row(KP k, float *row) {
+    for (int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; n < k.N;
+         n += (int64_t)gridDim.x * blockDim.x) {
+        int rk, j;
+        row[n] = box_of(k, n, rk, j) ? box_value(k, n, rk, j) : 0.0f;
     }
 }
 
@@ -664,7 +709,9 @@ template <int L, int BATCH, int T, typename F, typename I>
 static int launch_single(const KP &k, hipStream_t st) {
     using SP = SinglePass<L, BATCH, T, F, I>;
     dim3 grid((k.p.nchan + BATCH - 1) / BATCH);
+    tk_begin(TK_SINGLE, st);
     k_single<SP, T><<<grid, dim3(T), 0, st>>>(k);
+    tk_end(st);
     LAUNCHCHK();
     return PSS_OK;
 }
@@ -674,12 +721,18 @@ static int launch_four(const KP &k, hipStream_t st) {
     using C = Cols<N1, B, T, CF, CI>;
     using R = Rows<N2, BR, TR, RF, RI>;
     dim3 gc((unsigned)(N2 / B), (unsigned)k.p.nchan);
+    tk_begin(TK_COLA, st);
     k_colA<C, T><<<gc, dim3(T), 0, st>>>(k);
+    tk_end(st);
     LAUNCHCHK();
     dim3 gr((unsigned)(N1 / BR), (unsigned)k.p.nchan);
+    tk_begin(TK_ROW, st);
     k_row<R, TR><<<gr, dim3(TR), 0, st>>>(k);
+    tk_end(st);
     LAUNCHCHK();
+    tk_begin(TK_COLC, st);
     k_colC<C, T><<<gc, dim3(T), 0, st>>>(k);
+    tk_end(st);
     LAUNCHCHK();
     return PSS_OK;
 }
@@ -760,6 +813,7 @@ static int run_single(KP &k, hipStream_t st) {
 
 static int run_fallback(KP &k, hipStream_t st) {
     dim3 g = stream_grid((k.N + 3) / 4, k.p.nchan);
+    tk_begin(TK_FALLBACK, st);
     k_fb_source<<<g, dim3(256), 0, st>>>(k);
     LAUNCHCHK();
     k_fb_twiddles<<<stream_grid(k.N, 1), dim3(256), 0, st>>>(k);
@@ -770,6 +824,7 @@ static int run_fallback(KP &k, hipStream_t st) {
     k_fb_dft<true><<<gd, dim3(256), 0, st>>>(k);
     LAUNCHCHK();
     k_fb_epilogue<<<g, dim3(256), 0, st>>>(k);
+    tk_end(st);
     LAUNCHCHK();
     return PSS_OK;
 }
@@ -794,8 +849,7 @@ static int validate(const PssPipeline *p) {
         if (p->nsamp & 1)
             return fail(PSS_EINVAL, "odd N=%lld: the reference's irfft returns N-1 samples", (long long)p->nsamp);
         if (!p->ramp || !p->nyq_re || !p->nyq_im) return fail(PSS_EINVAL, "shift needs ramp/nyq arrays");
-        if (!p->work && pss_workspace_bytes(p->nchan, p->nsamp) > 0)
-            return fail(PSS_EINVAL, "shift needs a workspace");
+        if (!p->work) return fail(PSS_EINVAL, "shift needs a workspace");
         if (p->nsamp > (1ll << 24) && !is_pow2(p->nsamp))
             return fail(PSS_EUNSUPPORTED, "N=%lld", (long long)p->nsamp);
     }
@@ -807,6 +861,25 @@ extern "C" {
 
 int pss_version(void) { return 100; }
 
+void pss_timing_enable(int on) {
+    g_timing = on != 0;
+}
+
+int pss_timing_collect(int32_t *kind, double *ms, int64_t *units, int cap) {
+    int n = 0;
+    for (int i = 0; i < g_ntl; ++i) {
+        TimedLaunch &t = g_tl[i];
+        float e = 0.f;
+        hipEventSynchronize(t.b);
+        hipEventElapsedTime(&e, t.a, t.b);
+        if (n < cap) { kind[n] = t.kind; ms[n] = e; units[n] = t.units; ++n; }
+        hipEventDestroy(t.a);
+        hipEventDestroy(t.b);
+    }
+    g_ntl = 0;
+    return n;
+}
+
 int pss_last_error(char *buf, size_t n) {
     if (buf && n) {
         strncpy(buf, g_err, n - 1);
@@ -815,10 +888,15 @@ int pss_last_error(char *buf, size_t n) {
     return (int)strlen(g_err);
 }
 
-int64_t pss_workspace_bytes(int32_t nchan, int64_t nsamp) {
+// Layout: [spill area][mask row: nsamp floats, 256-B aligned]
+static int64_t spill_bytes(int32_t nchan, int64_t nsamp) {
     const int64_t one = (int64_t)nchan * nsamp * 8;
     if (is_pow2(nsamp) && nsamp >= 64 && nsamp <= (1ll << 24)) return nsamp > 8192 ? one : 0;
     return 2 * one + nsamp * 8;   // fallback: W1, W2 and the twiddle table
+}
+
+int64_t pss_workspace_bytes(int32_t nchan, int64_t nsamp) {
+    return ((spill_bytes(nchan, nsamp) + 255) & ~255ll) + nsamp * 4;
 }
 
 int pss_run(const PssPipeline *p, void *stream) {
@@ -831,13 +909,23 @@ int pss_run(const PssPipeline *p, void *stream) {
     k.N1 = 1;
     k.N2 = p->nsamp;
     k.invN = (float)(1.0 / (double)p->nsamp);
+    g_tk_units = (int64_t)p->nchan * p->nsamp;
     if (!p->shift) {
         dim3 g = stream_grid((k.N + 3) / 4, p->nchan);
+        tk_begin(TK_ELEM, st);
         k_elementwise<<<g, dim3(256), 0, st>>>(k);
+        tk_end(st);
         LAUNCHCHK();
         return PSS_OK;
     }
     const int64_t N = p->nsamp;
+    if (p->null_mode == PSS_NULL_DELAYED && !p->inj_box) {
+        float *row = reinterpret_cast<float *>(reinterpret_cast<char *>(p->work) +
+                                               ((spill_bytes(p->nchan, N) + 255) & ~255ll));
+        k_box_row<<<stream_grid(N, 1), dim3(256), 0, st>>>(k, row);
+        LAUNCHCHK();
+        k.p.inj_box = row;
+    }
     if (is_pow2(N) && N >= 64 && N <= 8192) return run_single(k, st);
     if (is_pow2(N) && N >= 16384 && N <= (1ll << 24)) return run_fourstep(k, st);
     return run_fallback(k, st);

@@ -93,22 +93,25 @@ class ISM(object):
         full_profs = pulsar.Profiles.calc_profiles(np.linspace(0.0, 1.0, Nph), signal.Nchan)
         t = np.linspace(0, pulsar._P(), Nph)
         tails = np.zeros((signal.Nchan, Nph))
-        for ii, tau in enumerate(np.atleast_1d(tau_scaled)):
-            tails[ii, :] = np.exp(-t * 1e3 / tau)        # t [s] / tau [ms]
+        tau = np.atleast_1d(tau_scaled)
+        tails[:tau.size, :] = np.exp(-(t[None, :] * 1e3) / tau[:, None])   # t [s] / tau [ms]
         pulsar._Profiles = DataPortrait(self.convolve_profile(full_profs, tails, width=Nph))
 
     def convolve_profile(self, profiles, convolve_array, width=2048):
         """ism.py:243-288: per row, linear convolution of the sum-normalised
         profile with the sum-normalised kernel, first `width` samples,
         rescaled by the profile sum."""
-        for ii in range(convolve_array.shape[0]):
-            ps = np.sum(profiles[ii, :])
-            pn = profiles[ii, :] / ps if ps != 0.0 else profiles[ii, :]
-            ks = np.sum(convolve_array[ii, :])
-            kn = convolve_array[ii, :] / ks if ks != 0.0 else convolve_array[ii, :]
-            n = pn.size + kn.size - 1
-            conv = np.fft.irfft(np.fft.rfft(pn, n) * np.fft.rfft(kn, n), n)
-            profiles[ii, :] = ps * conv[:width]
+        prof = np.asarray(profiles, dtype=float)
+        kern = np.asarray(convolve_array, dtype=float)
+        rows = kern.shape[0]
+        ps = np.sum(prof[:rows], axis=1, keepdims=True)
+        pn = np.where(ps != 0.0, prof[:rows] / np.where(ps != 0.0, ps, 1.0), prof[:rows])
+        ks = np.sum(kern, axis=1, keepdims=True)
+        kn = np.where(ks != 0.0, kern / np.where(ks != 0.0, ks, 1.0), kern)
+        n = pn.shape[1] + kn.shape[1] - 1
+        nfft = 1 << int(np.ceil(np.log2(n)))           # linear convolution, zero padded
+        conv = np.fft.irfft(np.fft.rfft(pn, nfft, axis=1) * np.fft.rfft(kn, nfft, axis=1), nfft, axis=1)
+        profiles[:rows, :] = ps * conv[:, :width]
         return profiles
 
     def scale_dnu_d(self, dnu_d, nu_i, nu_f, beta=KOLMOGOROV_BETA):

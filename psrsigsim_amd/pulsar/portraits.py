@@ -33,61 +33,79 @@ def _edge_slope(h0, h1, m0, m1):
     return np.where((~flip) & big, 3 * m0, d)
 
 
-def pchip_slopes(x, y):
+def pchip_slopes(x, y, h=None, m=None):
     """Knot derivatives for rows of ``y`` (shape [rows, K]) at knots ``x``."""
     x = np.asarray(x, dtype=float)
     y = np.asarray(y, dtype=float)
-    h = np.diff(x)
-    m = np.diff(y, axis=1) / h
+    if h is None:
+        h = np.diff(x)
+    if m is None:
+        m = np.diff(y, axis=1) / h
     K = x.size
     if K == 2:
         return np.repeat(m, 2, axis=1)
-    d = np.zeros_like(y)
-    sm = np.sign(m)
-    flat = (sm[:, 1:] != sm[:, :-1]) | (m[:, 1:] == 0) | (m[:, :-1] == 0)
+    d = np.empty_like(y)
+    m0, m1 = m[:, :-1], m[:, 1:]
     w1 = 2 * h[1:] + h[:-1]
     w2 = h[1:] + 2 * h[:-1]
     with np.errstate(divide="ignore", invalid="ignore"):
-        whmean = (w1 / m[:, :-1] + w2 / m[:, 1:]) / (w1 + w2)
-        inner = 1.0 / whmean
-    d[:, 1:-1] = np.where(flat, 0.0, inner)
+        inner = 1.0 / ((w1 / m0 + w2 / m1) / (w1 + w2))
+    flat = (np.signbit(m0) != np.signbit(m1)) | (m1 == 0) | (m0 == 0)
+    inner[flat] = 0.0
+    d[:, 1:-1] = inner
     d[:, 0] = _edge_slope(h[0], h[1], m[:, 0], m[:, 1])
     d[:, -1] = _edge_slope(h[-1], h[-2], m[:, -1], m[:, -2])
     return d
 
 
 def pchip_coefficients(x, y):
-    """Piecewise-cubic coefficients c[4, K-1, rows] in (t - x_i) powers 3..0."""
+    """Piecewise-cubic coefficients [rows, K-1, 4] in powers (t - x_i)^(3..0)."""
     x = np.asarray(x, dtype=float)
     y = np.asarray(y, dtype=float)
-    d = pchip_slopes(x, y)
     h = np.diff(x)
     m = np.diff(y, axis=1) / h
-    t = (d[:, :-1] + d[:, 1:] - 2 * m) / h
-    c = np.empty((4, x.size - 1, y.shape[0]))
-    c[0] = (t / h).T
-    c[1] = ((m - d[:, :-1]) / h - t).T
-    c[2] = d[:, :-1].T
-    c[3] = y[:, :-1].T
+    d = pchip_slopes(x, y, h, m)
+    d0, d1 = d[:, :-1], d[:, 1:]
+    t = (d0 + d1 - 2 * m) / h
+    c = np.empty((y.shape[0], x.size - 1, 4))
+    c[:, :, 0] = t / h
+    c[:, :, 1] = (m - d0) / h - t
+    c[:, :, 2] = d0
+    c[:, :, 3] = y[:, :-1]
     return c
 
 
-def ppoly_eval(x, c, ph):
-    """Evaluate the piecewise cubic at phases ``ph`` (extrapolating with the end
-    pieces); returns [rows, len(ph)]."""
+def ppoly_eval(x, c, ph, y=None):
+    """Evaluate the piecewise cubic at phases ``ph`` (extrapolating with the
+    end pieces); returns [rows, len(ph)].  Phases that are exactly the first
+    len(ph) knots return the knot values ``y`` (t = 0 exactly)."""
     ph = np.asarray(ph, dtype=float)
+    if y is not None and ph.size <= x.size and np.array_equal(ph, x[:ph.size]):
+        return np.array(y[:, :ph.size])
     i = np.clip(np.searchsorted(x, ph, side="right") - 1, 0, x.size - 2)
-    t = ph - x[i]
-    out = c[0, i] * t[:, None]
-    out = (out + c[1, i]) * t[:, None]
-    out = (out + c[2, i]) * t[:, None]
-    out = out + c[3, i]
-    return out.T
+    t = (ph - x[i])[None, :]
+    ci = c[:, i, :]
+    out = ci[:, :, 0] * t
+    out += ci[:, :, 1]
+    out *= t
+    out += ci[:, :, 2]
+    out *= t
+    out += ci[:, :, 3]
+    return out
 
 
 # ---------------------------------------------------------------------------
 # portraits
 # ---------------------------------------------------------------------------
+def _first_max_row(profiles):
+    """``[pr for pr in profiles if pr.max() == 1.0][0]`` (portraits.py:45),
+    vectorised; IndexError when no row peaks at exactly 1.0, as there."""
+    hit = np.flatnonzero(np.max(profiles, axis=1) == 1.0)
+    if hit.size == 0:
+        raise IndexError("list index out of range")
+    return profiles[hit[0]]
+
+
 class PulsePortrait(object):
     """portraits.py:9-91."""
     _profiles = None
@@ -105,7 +123,7 @@ class PulsePortrait(object):
         self._profiles = self.calc_profiles(ph, Nchan=Nchan)
         self._Amax = self._profiles.max()
         self._profiles = self._profiles / self.Amax
-        self._max_profile = [pr for pr in self._profiles if pr.max() == 1.0][0]
+        self._max_profile = _first_max_row(self._profiles)
 
     def calc_profiles(self, phases, Nchan=None):
         raise NotImplementedError()
@@ -163,7 +181,7 @@ class GaussPortrait(PulsePortrait):
         """portraits.py:131-140 (no renormalisation)."""
         ph = np.arange(Nphase) / Nphase
         self._profiles = self.calc_profiles(ph, Nchan=Nchan)
-        self._max_profile = [pr for pr in self._profiles if pr.max() == 1.0][0]
+        self._max_profile = _first_max_row(self._profiles)
 
     def calc_profiles(self, phases, Nchan=None):
         ph = np.array(phases)
@@ -205,14 +223,13 @@ class DataPortrait(PulsePortrait):
 
     def __init__(self, profiles, phases=None):
         profiles = np.asarray(profiles)
-        if np.any(profiles < 0.0):
+        neg = profiles < 0.0
+        if np.any(neg):
             log.warning("Some phase bins of input profile are negative, replacing them with zeros...")
-            for prof in profiles:
-                if np.any(prof < 0.0):
-                    prof[np.where(prof < 0.0)[0]] = 0.0
+            profiles[neg] = 0.0        # in place on the caller's array, as there
         if phases is None:
             N = profiles.shape[1]
-            if any(a != b for a, b in zip(profiles[:, 0], profiles[:, -1])):
+            if np.any(profiles[:, 0] != profiles[:, -1]):
                 profiles = np.append(profiles, profiles[:, 0][:, np.newaxis], axis=1)
                 phases = np.arange(N + 1) / N
             else:
@@ -222,14 +239,14 @@ class DataPortrait(PulsePortrait):
             if phases[-1] != 1:
                 phases = np.append(phases, 1)
                 profiles = np.append(profiles, profiles[:, 0][:, np.newaxis], axis=1)
-            elif any(a != b for a, b in zip(profiles[:, 0], profiles[:, -1])):
+            elif np.any(profiles[:, 0] != profiles[:, -1]):
                 profiles[:, -1] = profiles[:, 0]
         self._knots = np.asarray(phases, dtype=float)
         self._kvals = np.asarray(profiles, dtype=float)
         self._coef = pchip_coefficients(self._knots, self._kvals)
 
     def _generator(self, phases):
-        return ppoly_eval(self._knots, self._coef, phases)
+        return ppoly_eval(self._knots, self._coef, phases, self._kvals)
 
     def calc_profiles(self, phases, Nchan=None):
         profiles = self._generator(phases)
@@ -256,9 +273,9 @@ class DataPortrait(PulsePortrait):
         M, nint = geo
         h = 1.0 / M
         amax = self.Amax if hasattr(self, '_Amax') else 1.0
-        c = self._coef  # [4, nint, rows]
-        tab = np.stack([c[0] * h ** 3, c[1] * h ** 2, c[2] * h, c[3]], axis=-1)  # [nint, rows, 4]
-        tab = np.transpose(tab, (1, 0, 2)) / amax
+        tab = self._coef * np.array([h ** 3, h ** 2, h, 1.0])     # [rows, nint, 4]
+        if amax != 1.0:
+            tab = tab / amax
         return np.ascontiguousarray(tab, dtype=np.float32), M, nint
 
 

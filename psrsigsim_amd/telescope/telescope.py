@@ -99,16 +99,19 @@ class Telescope(object):
         odt = torch.int8 if signal.dtype is np.int8 else torch.float32
         okind = _lib.OUT_I8 if signal.dtype is np.int8 else _lib.OUT_F32
         clip = float(signal._draw_max) if signal._draw_max is not None else float("inf")
-        if kind == "copy":
+        # The reference always builds `out` but only returns it on request;
+        # here it is produced only when it is observable (ret_resampsig).
+        out = None
+        if ret_resampsig and kind == "copy":
             out = torch.empty((rows, ncols), dtype=odt, device=dev)
             pend.out = {"kind": okind, "tensor": out, "clip": clip}
-        else:
+        elif ret_resampsig:
             pre = torch.empty((rows, ncols), dtype=torch.float32, device=dev)
             pend.out = {"kind": _lib.OUT_F32, "tensor": pre, "clip": float("inf")}
         if noise:
             rcvr.radiometer_noise(signal, pulsar, gain=self.gain, Tsys=self.Tsys)
         signal._flush()
-        if kind != "copy":
+        if ret_resampsig and kind != "copy":
             if kind == "down":
                 new_Nt = int(signal.nsamp // arg)
                 if ncols % arg or ncols // arg != new_Nt:

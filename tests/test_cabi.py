@@ -32,9 +32,11 @@ def test_library_loads_and_exports_everything():
 
 def test_workspace_sizes():
     L = _lib.load()
-    assert L.pss_workspace_bytes(4, 4096) == 0            # single pass, LDS only
-    assert L.pss_workspace_bytes(4, 1 << 20) == 4 * (1 << 20) * 8
-    assert L.pss_workspace_bytes(2, 244) == 2 * 2 * 244 * 8 + 244 * 8   # fallback
+    # [spill area, 256-B aligned][null mask row: nsamp floats]
+    assert L.pss_workspace_bytes(4, 4096) == 4096 * 4               # single pass: LDS only
+    assert L.pss_workspace_bytes(4, 1 << 20) == 4 * (1 << 20) * 8 + (1 << 20) * 4
+    sp = 2 * 2 * 244 * 8 + 244 * 8                                   # fallback W1, W2, twiddles
+    assert L.pss_workspace_bytes(2, 244) == ((sp + 255) // 256) * 256 + 244 * 4
 
 
 def test_struct_layout_matches_header(tmp_path):
