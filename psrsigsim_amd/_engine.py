@@ -170,107 +170,92 @@ class Pending(object):
                 and self.noise is None and self.out is None)
 
 
-def build_pipeline(sig, pend, rows, chan0, data, out=None, global_rows=None):
-    """A PssPipeline for local rows [0, rows) whose global channels start at
-    ``chan0`` (or are listed in ``global_rows``).  Returns (struct, keepalive)."""
+def plan_pipeline(sig, pend, rows, chan0):
+    """Host-side plan of one fused run over global channels [chan0, chan0+rows):
+    every scalar field of PssPipeline plus the per-row numpy arrays (ramp
+    words, Nyquist factors, injected draws).  Pure host code (tested on CPU)."""
     N = sig._ncols
-    p = _lib.PssPipeline()
-    keep = []
-    gidx = np.arange(chan0, chan0 + rows) if global_rows is None else np.asarray(global_rows)
-    p.nchan = rows
-    p.chan0 = int(gidx[0])
-    p.nsamp = N
-    p.ld = data.stride(0)
-    p.data = ptr(data)
-    p.seed = _state["seed"]
+    gidx = np.arange(chan0, chan0 + rows)
+    P = {"nchan": rows, "chan0": int(chan0), "nsamp": N, "seed": _state["seed"], "arrays": {}}
+    A = P["arrays"]
     src = pend.source
     if src is None:
-        p.src = _lib.SRC_LOAD
+        P["src"] = _lib.SRC_LOAD
     else:
-        p.src = _lib.SRC_SEARCH if src.mode == "search" else _lib.SRC_FOLD
-        # rows are indexed by GLOBAL channel inside the kernel (or row 0 when
-        # the table is shared); the device copy is cached on the stage.
-        if getattr(src, "dev_table", None) is None:
-            src.dev_table = to_dev(src.table)
-        tt = src.dev_table
-        p.prof_rows = src.table.shape[0]
-        p.prof = ptr(tt)
-        p.nint = src.nint
-        p.nph = src.nph
-        p.phase_step = src.phase_step
-        p.knot_m = src.M
-        p.gen_df = src.df
-        p.draw_norm = src.draw_norm
-        p.call_gen = src.call_id
+        P.update(src=_lib.SRC_SEARCH if src.mode == "search" else _lib.SRC_FOLD,
+                 prof_rows=src.table.shape[0], nint=src.nint, nph=src.nph,
+                 phase_step=src.phase_step, knot_m=src.M, gen_df=src.df,
+                 draw_norm=src.draw_norm, call_gen=src.call_id)
         if src.inj is not None:
-            t = to_dev(np.asarray(src.inj, dtype=np.float32)[gidx])
-            keep.append(t)
-            p.inj_gen = ptr(t)
-    need_fft = bool(pend.shifts) or (pend.null is not None and pend.null["mode"] == "delayed")
+            A["inj_gen"] = np.asarray(src.inj, dtype=np.float32)[gidx]
+    nul = pend.null
+    need_fft = bool(pend.shifts) or (nul is not None and nul["mode"] == "delayed")
     if need_fft:
         if N % 2:
             raise ValueError("could not broadcast input array from shape (%d,) into shape (%d,)"
                              % (N - 1, N))
-        p.shift = 1
+        P["shift"] = 1
         total = np.zeros(sig.Nchan)
         nyq_re = np.ones(sig.Nchan)
-        for s in pend.shifts:
-            total = total + s
-            nyq_re = nyq_re * np.cos(np.pi * s)
-        nul = pend.null
+        for sh in pend.shifts:
+            total = total + sh
+            nyq_re = nyq_re * np.cos(np.pi * sh)
         if nul is not None and nul["mode"] == "delayed":
             mask_total = nul["mask_samples"]
             nyq_im = np.cos(np.pi * mask_total)
             if pend.shifts:
-                p.data_in_fft = 1
-                ramp_s = total
+                P["data_in_fft"], ramp_s = 1, total
             else:
-                p.data_in_fft = 0
-                ramp_s = mask_total
+                P["data_in_fft"], ramp_s = 0, mask_total
         else:
-            p.data_in_fft = 1
-            ramp_s = total
-            nyq_im = nyq_re
-        r = u64_to_i64_tensor(ramp_words(ramp_s[gidx], N))
-        a = to_dev(nyq_re[gidx].astype(np.float32))
-        b = to_dev(nyq_im[gidx].astype(np.float32))
-        keep += [r, a, b]
-        p.ramp, p.nyq_re, p.nyq_im = ptr(r), ptr(a), ptr(b)
-        wb = _lib.load().pss_workspace_bytes(rows, N)
-        ws = workspace(wb)
-        p.work = ptr(ws) if ws is not None else None
-    nul = pend.null
+            P["data_in_fft"], ramp_s, nyq_im = 1, total, nyq_re
+        A["ramp"] = ramp_words(ramp_s[gidx], N)
+        A["nyq_re"] = nyq_re[gidx].astype(np.float32)
+        A["nyq_im"] = nyq_im[gidx].astype(np.float32)
     if nul is not None:
-        p.null_mode = _lib.NULL_DELAYED if nul["mode"] == "delayed" else _lib.NULL_UNDELAYED
-        rk = to_dev(nul["rank"].astype(np.int32))
-        keep.append(rk)
-        p.null_rank = ptr(rk)
-        p.null_slots = int(nul["rank"].size)
-        p.null_shift = int(nul["shift_val"])
-        p.nph = int(nul["nph"])
-        p.null_box_df = nul["box_df"]
-        p.null_box_scale = nul["box_scale"]
-        p.null_rep_df = nul.get("rep_df", 1.0)
-        p.null_rep_scale = nul.get("rep_scale", 0.0)
-        p.call_null = nul["call_id"]
+        P.update(null_mode=_lib.NULL_DELAYED if nul["mode"] == "delayed" else _lib.NULL_UNDELAYED,
+                 null_slots=int(nul["rank"].size), null_shift=int(nul["shift_val"]),
+                 nph=int(nul["nph"]), null_box_df=nul["box_df"], null_box_scale=nul["box_scale"],
+                 null_rep_df=nul.get("rep_df", 1.0), null_rep_scale=nul.get("rep_scale", 0.0),
+                 call_null=nul["call_id"])
+        A["null_rank"] = nul["rank"].astype(np.int32)
         if nul.get("inj_box") is not None:
-            t = to_dev(np.asarray(nul["inj_box"], dtype=np.float32))
-            keep.append(t)
-            p.inj_box = ptr(t)
+            A["inj_box"] = np.asarray(nul["inj_box"], dtype=np.float32)
         if nul.get("inj_rep") is not None:
-            t = to_dev(np.asarray(nul["inj_rep"], dtype=np.float32)[gidx])
-            keep.append(t)
-            p.inj_rep = ptr(t)
+            A["inj_rep"] = np.asarray(nul["inj_rep"], dtype=np.float32)[gidx]
     noi = pend.noise
     if noi is not None:
-        p.noise = 1
-        p.noise_df = noi["df"]
-        p.noise_norm = noi["norm"]
-        p.call_noise = noi["call_id"]
+        P.update(noise=1, noise_df=noi["df"], noise_norm=noi["norm"], call_noise=noi["call_id"])
         if noi.get("inj") is not None:
-            t = to_dev(np.asarray(noi["inj"], dtype=np.float32)[gidx])
-            keep.append(t)
-            p.inj_noise = ptr(t)
+            A["inj_noise"] = np.asarray(noi["inj"], dtype=np.float32)[gidx]
+    return P
+
+
+def build_pipeline(sig, pend, rows, chan0, data, out=None):
+    """A PssPipeline (plus the device buffers it points at) for local rows
+    [0, rows) of ``data`` holding global channels [chan0, chan0+rows)."""
+    P = plan_pipeline(sig, pend, rows, chan0)
+    p = _lib.PssPipeline()
+    keep = []
+    for k, v in P.items():
+        if k != "arrays":
+            setattr(p, k, v)
+    p.ld = data.stride(0)
+    p.data = ptr(data)
+    src = pend.source
+    if src is not None:
+        # rows are indexed by GLOBAL channel inside the kernel (or row 0 when
+        # the table is shared); the device copy is cached on the stage.
+        if getattr(src, "dev_table", None) is None:
+            src.dev_table = to_dev(src.table)
+        p.prof = ptr(src.dev_table)
+    for name, arr in P["arrays"].items():
+        t = u64_to_i64_tensor(arr) if name == "ramp" else to_dev(arr)
+        keep.append(t)
+        setattr(p, name, ptr(t))
+    if P.get("shift"):
+        ws = workspace(_lib.load().pss_workspace_bytes(rows, sig._ncols))
+        p.work = ptr(ws) if ws is not None else None
     if out is not None:
         p.out_kind = out["kind"]
         p.out = ptr(out["tensor"])

@@ -1,0 +1,127 @@
+"""Stochastic stages on the GPU (Philox draws): distributions against the
+reference's (chi2 via scipy), per-channel moments against the CPU oracle, and
+shard invariance (a sharded run reproduces the unsharded rows bit for bit)."""
+import numpy as np
+import pytest
+import torch
+from scipy import stats
+
+from oracle import pss_cpu as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _fill(df, rows=2, n=1 << 20, purpose=5, call=7):
+    from psrsigsim_amd import _lib, _engine
+    out = torch.empty((rows, n), dtype=torch.float32, device="cuda")
+    rc = _lib.lib().pss_chi2_fill(_engine.ptr(out), rows, 0, n, float(df), 1234, call, purpose,
+                                  _engine.stream_ptr())
+    _lib.check(rc)
+    return out.cpu().numpy().astype(np.float64)
+
+
+@pytest.mark.parametrize("df", [1.0, 0.5, 3.7, 100.0, 11190.0])
+def test_chi2_draws_distribution(df, hip_lib):
+    x = _fill(df)
+    for row in x:
+        m, v = row.mean(), row.var()
+        assert abs(m / df - 1) < 5e-3, (df, m)
+        assert abs(v / (2 * df) - 1) < 1e-2, (df, v)
+        p = stats.kstest(row[:200000], stats.chi2(df).cdf).pvalue
+        assert p > 0.01, (df, p)
+
+
+def test_chi2_streams_independent(hip_lib):
+    a = _fill(1.0, call=1)[0]
+    b = _fill(1.0, call=2)[0]
+    assert abs(np.corrcoef(a[:100000], b[:100000])[0, 1]) < 0.02
+
+
+def _c3_small(nchan, shard, log2n=16, noise=True, seed=5):
+    import psrsigsim_amd as pss
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+    from psrsigsim_amd.ism import ISM
+    from psrsigsim_amd.telescope import telescope as T
+    pss.seed(seed)
+    sig = FilterBankSignal(1400, 400, Nsubband=nchan, fold=False, shard=shard)
+    psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
+    ism = ISM()
+    ism.scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
+    psr.make_pulses(sig, tobs=(1 << log2n) * 20.48e-6)
+    ism.disperse(sig, 100)
+    psr.null(sig, 0.1)
+    T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=noise)
+    return sig.data.cpu().numpy()
+
+
+@pytest.mark.parametrize("log2n", [13, 16])
+def test_shard_invariance_bitwise(log2n, hip_lib):
+    full = _c3_small(8, None, log2n)
+    a = _c3_small(8, (0, 3), log2n)
+    b = _c3_small(8, (3, 8), log2n)
+    np.testing.assert_array_equal(np.vstack([a, b]), full)
+
+
+def test_pulse_and_noise_moments_vs_oracle(hip_lib):
+    """Per-channel mean and variance of the final C3-style signal (Philox)
+    against the oracle (legacy RandomState) within 0.5 % + sampling error."""
+    log2n = 20
+    g = _c3_small(2, None, log2n)
+    sig = O.Signal(1400, 400, nchan=2, fold=False)
+    psr = O.Pulsar(0.005, 1.0, profiles=O.GaussPortrait(0.5, 0.05, 1))
+    d = O.LegacyDraws(3)
+    O.scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
+    O.make_pulses(sig, psr, (1 << log2n) * 20.48e-6, d)
+    O.disperse(sig, 100)
+    O.null(sig, psr, 0.1, d)
+    O.observe(sig, psr, O.Arecibo(), "Lband_PUPPI", d, noise=True)
+    for c in range(2):
+        x, y = g[c].astype(np.float64), sig.data[c]
+        n = x.size
+        for stat, se in ((np.mean, lambda a: a.std() / np.sqrt(n)),
+                         (np.var, lambda a: np.sqrt(np.mean((a - a.mean()) ** 4) / n))):
+            sx, sy = stat(x), stat(y)
+            tol = max(5e-3 * abs(sy), 5 * np.hypot(se(x), se(y)))
+            assert abs(sx - sy) <= tol, (c, stat.__name__, sx, sy, tol)
+
+
+def test_search_pulse_draws_are_chi2_1(hip_lib):
+    """make_pulses alone (no delay): data / PCHIP(phase) ~ chi2(1)."""
+    import psrsigsim_amd as pss
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+    pss.seed(11)
+    sig = FilterBankSignal(1400, 400, Nsubband=2, fold=False)
+    psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.1, 1))
+    psr.make_pulses(sig, tobs=(1 << 18) * 20.48e-6)
+    x = sig.data.cpu().numpy().astype(np.float64)
+    spp = (sig._samprate_MHz() * 0.005) * 1e6
+    ph = (np.arange(x.shape[1]) / spp) % 1
+    prof = psr.Profiles.calc_profiles(ph)
+    sel = prof[0] > 0.5
+    r = x[0, sel] / prof[0, sel]
+    assert stats.kstest(r[:200000], stats.chi2(1).cdf).pvalue > 0.01
+    assert abs(r.mean() - 1) < 1e-2
+
+
+def test_radiometer_noise_distribution(hip_lib):
+    """observe(noise=True): (after - before) / norm ~ chi2(df)."""
+    import psrsigsim_amd as pss
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+    from psrsigsim_amd.telescope import telescope as T
+    from psrsigsim_amd.telescope.receiver import Receiver
+    pss.seed(12)
+    sig = FilterBankSignal(1400, 400, Nsubband=2, sublen=0.05)
+    psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
+    psr.make_pulses(sig, tobs=1.0)
+    before = sig.data.cpu().numpy().astype(np.float64)
+    tel = T.Arecibo()
+    tel.observe(sig, psr, system="Lband_PUPPI", noise=True)
+    after = sig.data.cpu().numpy().astype(np.float64)
+    norm = Receiver.noise_norm(sig, psr, tel.Tsys, tel.gain)
+    df = float(sig.Nfold)
+    z = ((after - before) / norm).ravel()
+    assert abs(z.mean() / df - 1) < 5e-3
+    assert stats.kstest(z, stats.chi2(df).cdf).pvalue > 0.01

@@ -1,0 +1,170 @@
+"""CPU checks of the host plan layer against the reference's golden vectors:
+derived integers/scalars (nsamp, nsub, Nfold, Smax, draw_norm), channel
+frequencies, accumulated delays, the device PCHIP table (evaluated on the
+host exactly as the kernel does), the radiometer noise scale and observe's
+branch decisions.  No GPU needed (stages are only recorded, not run)."""
+import numpy as np
+import pytest
+
+from oracle import pss_cpu as O
+from tests import replay
+from tests.fixtures_util import load
+
+
+def _product(name):
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, GaussProfile, DataProfile
+    case = replay.CASES[name]
+    sg = case["sig"]
+    sig = FilterBankSignal(sg["fcent"], sg["bw"], Nsubband=sg["nchan"], sample_rate=sg.get("samprate"),
+                           sublen=sg.get("sublen"), dtype=sg.get("dtype", np.float32),
+                           fold=sg.get("fold", True))
+    ps = case["psr"]
+    spec = ps["prof"]
+    if spec[0] == "gauss":
+        prof = GaussProfile(*spec[1:])
+    elif spec[0] == "gaussarr":
+        prof = GaussProfile(np.array([0.3, 0.6]), np.array([0.02, 0.05]), np.array([0.5, 1.0]))
+    else:
+        prof = DataProfile(replay._prof(), Nchan=spec[1])
+    psr = Pulsar(ps["period"], ps["Smean"], profiles=prof, specidx=ps.get("specidx", 0.0),
+                 ref_freq=ps.get("ref_freq"))
+    return case, sig, psr
+
+
+@pytest.mark.parametrize("name", sorted(replay.CASES))
+def test_derived_quantities(name):
+    from psrsigsim_amd.ism import ISM
+    meta, A, _ = load(name)
+    case, sig, psr = _product(name)
+    ism = ISM()
+    for op in case["ops"]:
+        if op[0] == "scatter_conv":
+            ism.scatter_broaden(sig, op[1], op[2], convolve=True, pulsar=psr)
+        elif op[0] == "make_pulses":
+            psr.make_pulses(sig, op[1])
+            break
+    assert sig.nsamp == meta["nsamp"] and sig.nsub == meta["nsub"]
+    if meta.get("Nfold") is not None:
+        assert np.isclose(float(sig.Nfold), meta["Nfold"], rtol=1e-12)
+    assert np.isclose(float(sig._Smax.value), meta["Smax"], rtol=1e-12)
+    assert np.isclose(sig._draw_norm, meta["draw_norm"], rtol=1e-12)
+    assert sig._draw_max == meta["draw_max"]
+    np.testing.assert_array_equal(sig.dat_freq.value, A["dat_freq"])
+    assert sig._ncols == A["data_pulses"].shape[1]
+    np.testing.assert_allclose(psr.Profiles._max_profile, A["max_profile"], rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize("name", ["northstar_mini", "j1713_search", "null_undelayed"])
+def test_device_pchip_table_matches_reference_generator(name):
+    """The fp32 table the kernel evaluates (local coordinate u) reproduces the
+    reference's PchipInterpolator coefficients (recorded) at every sample."""
+    meta, A, _ = load(name)
+    case, sig, psr = _product(name)
+    from psrsigsim_amd.ism import ISM
+    for op in case["ops"]:
+        if op[0] == "scatter_conv":
+            ISM().scatter_broaden(sig, op[1], op[2], convolve=True, pulsar=psr)
+        elif op[0] == "make_pulses":
+            psr.make_pulses(sig, op[1])
+            break
+    src = sig._pending.source
+    tab = src.table.astype(np.float64)
+    n = np.arange(sig._ncols, dtype=np.uint64)
+    ph = (n * np.uint64(src.phase_step)).astype(np.uint64)          # wrapping, like the kernel
+    hi = ((ph >> np.uint64(32)).astype(np.float64) * src.M) / 2.0 ** 32
+    iv = np.minimum(np.floor(hi).astype(np.int64), src.nint - 1)
+    u = hi - iv
+    rows = tab[np.zeros(1, int) if tab.shape[0] == 1 else np.arange(tab.shape[0])]
+    c = rows[:, iv, :]
+    val = ((c[..., 0] * u + c[..., 1]) * u + c[..., 2]) * u + c[..., 3]
+    # reference: data_pulses = PCHIP(phase) * chi2 draw  -> divide the draws out
+    draws = load(name)[2][0][2]
+    ref = A["data_pulses"] / draws
+    np.testing.assert_allclose(np.broadcast_to(val, ref.shape), ref, rtol=0, atol=2e-6 * np.max(ref))
+
+
+@pytest.mark.parametrize("name", ["tutorial1", "northstar_mini", "fold_sublen", "specidx_int8"])
+def test_delays_and_noise_scale(name):
+    from psrsigsim_amd.ism import ISM
+    from psrsigsim_amd.telescope import telescope as T
+    from psrsigsim_amd.telescope.receiver import Receiver
+    meta, A, draws = load(name)
+    case, sig, psr = _product(name)
+    ism = ISM()
+    mo, Ao, inj = replay.oracle_run(name)   # oracle (pinned) for the noise scale
+    for op in case["ops"]:
+        k = op[0]
+        if k == "scatter_conv":
+            ism.scatter_broaden(sig, op[1], op[2], convolve=True, pulsar=psr)
+        elif k == "make_pulses":
+            psr.make_pulses(sig, op[1])
+        elif k == "disperse":
+            ism.disperse(sig, op[1])
+        elif k == "fd":
+            ism.FD_shift(sig, op[1])
+        elif k == "scatter_shift":
+            ism.scatter_broaden(sig, op[1], op[2], convolve=False)
+    np.testing.assert_allclose(sig.delay.value, A["delay_ms"], rtol=1e-13)
+    tel = T.Arecibo() if "Arecibo" in str(case["ops"][-1]) else T.GBT()
+    norm = Receiver.noise_norm(sig, psr, tel.Tsys, tel.gain)
+    ref_noise = (A["data_noise"] - (A["data_null"] if "data_null" in A else A["data_disperse"]))
+    ref_norm = np.median(ref_noise / draws[-1][2])
+    assert np.isclose(norm, ref_norm, rtol=1e-9), (norm, ref_norm)
+
+
+@pytest.mark.parametrize("tag,kind", [("eq", "copy"), ("down", "down"), ("rebin", "rebin")])
+def test_observe_branch_decisions(tag, kind):
+    from psrsigsim_amd.telescope import Telescope, Backend
+    from psrsigsim_amd._units import Quantity
+    case, sig, psr = _product("observe_" + tag)
+    psr.make_pulses(sig, 0.02)
+    dt = case["ops"][-1][1][1]
+    got, _ = Telescope.resample_branch(sig, Backend(samprate=1.0 / Quantity(dt, "s")))
+    assert got == kind
+
+
+def test_dataprofile_nchan_mismatch_raises():
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, DataProfile
+    sig = FilterBankSignal(1500, 800, Nsubband=4, sample_rate=0.048828125, fold=False)
+    psr = Pulsar(1.0 / 218.8118437960826270, 0.009, profiles=DataProfile(replay._prof()))
+    with pytest.raises(ValueError):
+        psr.make_pulses(sig, 4096 * 20.48e-6)
+
+
+def test_disperse_twice_raises():
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar
+    from psrsigsim_amd.ism import ISM
+    sig = FilterBankSignal(1400, 400, Nsubband=2, fold=False)
+    Pulsar(0.005, 1.0).make_pulses(sig, 4096 * 20.48e-6)
+    ism = ISM()
+    ism.disperse(sig, 10)
+    assert sig.dm.value == 10
+    with pytest.raises(ValueError):
+        ism.disperse(sig, 10)
+
+
+def test_receiver_errors():
+    from psrsigsim_amd.telescope import Receiver
+    from psrsigsim_amd.telescope.receiver import _flat_response
+    with pytest.raises(ValueError):
+        Receiver(fcent=None, bandwidth=400, name="Lband")
+    with pytest.raises(NotImplementedError):
+        Receiver(response=_flat_response(1400, 400), name="Lband")
+
+
+def test_pchip_matches_scipy():
+    from scipy.interpolate import PchipInterpolator
+    from psrsigsim_amd.pulsar.portraits import pchip_coefficients, ppoly_eval
+    rng = np.random.default_rng(0)
+    x = np.arange(245) / 244
+    y = rng.random((6, 245))
+    y[:, 3] = y[:, 4]
+    y[1, 10:20] = 0.3
+    y[2] = np.maximum(0, np.sin(6 * x))
+    c = pchip_coefficients(x, y)
+    P = PchipInterpolator(x, y, axis=1)
+    ph = np.linspace(-0.01, 1.02, 2000)
+    np.testing.assert_allclose(ppoly_eval(x, c, ph), P(ph), rtol=0, atol=1e-13)

@@ -1,0 +1,88 @@
+"""Multi-process (gloo, CPU) checks of the channel-sharded path: every rank
+plans its block of a sharded signal exactly like the same rows of the
+unsharded signal (tables, ramp words, Nyquist factors, RNG keys), so the
+device runs are bit-identical per row (the GPU side of that claim is
+tests/test_gpu_stats.py::test_shard_invariance_bitwise)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _plan(nchan, shard):
+    import psrsigsim_amd as pss
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+    from psrsigsim_amd.ism import ISM
+    from psrsigsim_amd import _engine
+    pss.seed(99)
+    sig = FilterBankSignal(1400, 400, Nsubband=nchan, fold=False, shard=shard)
+    psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
+    ism = ISM()
+    ism.scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
+    psr.make_pulses(sig, tobs=(1 << 16) * 20.48e-6)
+    ism.disperse(sig, 100)
+    ism.FD_shift(sig, [1e-4, 2e-5])
+    c0, c1 = sig.shard
+    P = _engine.plan_pipeline(sig, sig._pending, c1 - c0, c0)
+    return sig, P
+
+
+def _worker(rank, world, port, nchan, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    per = nchan // world
+    sig, P = _plan(nchan, (rank * per, (rank + 1) * per))
+    full_sig, F = _plan(nchan, None)
+    ok = True
+    sl = slice(rank * per, (rank + 1) * per)
+    for k in ("ramp", "nyq_re", "nyq_im"):
+        ok &= np.array_equal(P["arrays"][k], F["arrays"][k][sl])
+    for k in ("seed", "call_gen", "phase_step", "knot_m", "nint", "prof_rows", "draw_norm", "src"):
+        ok &= P[k] == F[k]
+    ok &= np.array_equal(sig._pending.source.table, full_sig._pending.source.table)
+    ok &= P["chan0"] == rank * per and P["nchan"] == per
+    # gather the shard plans on every rank: they tile the full plan exactly
+    t = torch.tensor(P["arrays"]["ramp"].view(np.int64))
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    whole = torch.cat(parts).numpy().view(np.uint64)
+    ok &= np.array_equal(whole, F["arrays"]["ramp"])
+    flag = torch.tensor([1 if ok else 0])
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        q.put(int(flag.item()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_plans_tile_the_unsharded_plan(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 16, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) == 1
+
+
+def test_shard_validation():
+    from psrsigsim_amd.signal import FilterBankSignal
+    with pytest.raises(ValueError):
+        FilterBankSignal(1400, 400, Nsubband=8, shard=(4, 12))
