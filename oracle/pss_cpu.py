@@ -345,6 +345,7 @@ def null(sig, psr, null_frac, draws, length=None, frequency=None):
     opm = np.mean(psr.Profiles._max_profile[opw.astype(int)])
     box_row = np.zeros(N)          # test-side record of the (pre-shift) box values
     rep_dense = None
+    mask_shifted = None
     if sig.delay is None:
         for p in pulses:
             bins = np.arange(Nph * p, Nph * (p + 1)) + shift_val
@@ -362,13 +363,14 @@ def null(sig, psr, null_frac, draws, length=None, frequency=None):
         dt_ms = (1.0 / sig.samprate) * 1e-3     # (1/samprate).to('ms')
         for c in range(sig.nchan):
             mask[c, :] = shift_t(mask[c, :], sig.delay[c], dt=dt_ms)
+        mask_shifted = mask
         hit = np.where(mask > 1)
         noise = draws.chi2(df, np.shape(hit)[1]) * sig.draw_norm
         sig.data[hit] = noise * opm
         rep_dense = np.zeros(sig.data.shape)
         rep_dense[hit] = noise * opm
     return {"shift_val": shift_val, "pulses": pulses, "opw": opw, "opm": opm,
-            "box_row": box_row, "rep_dense": rep_dense}
+            "box_row": box_row, "rep_dense": rep_dense, "mask_shifted": mask_shifted}
 
 
 # ---------------------------------------------------------------------------

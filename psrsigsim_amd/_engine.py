@@ -279,13 +279,15 @@ def execute(sig, pend):
             raise RuntimeError("signal has no data")
         sig._buf = torch.empty((rows, N), dtype=torch.float32, device=device())
     out = pend.out
-    if sig._c0 > 0 and sig._track_row0:
-        # shadow of global channel 0 (shard-invariant null()): same stages
-        if sig._row0 is None or sig._row0.shape[1] != N:
+    if (sig._c0 > 0 or sig._c1 < min(2, sig.Nchan)) and sig._track_row0:
+        # shadow of global channels 0..1 (shard-invariant null()): same stages,
+        # same (0, 1) channel pairing as the shard that owns channel 0
+        nrow = min(2, sig.Nchan)
+        if sig._row0 is None or tuple(sig._row0.shape) != (nrow, N):
             if pend.source is None:
                 raise RuntimeError("channel-0 shadow lost")
-            sig._row0 = torch.empty((1, N), dtype=torch.float32, device=device())
-        p0, k0 = build_pipeline(sig, pend, 1, 0, sig._row0)
+            sig._row0 = torch.empty((nrow, N), dtype=torch.float32, device=device())
+        p0, k0 = build_pipeline(sig, pend, nrow, 0, sig._row0)
         run(p0, k0)
     p, keep = build_pipeline(sig, pend, rows, sig._c0, sig._buf, out=out)
     run(p, keep)
@@ -293,22 +295,25 @@ def execute(sig, pend):
 
 def probe_row0(sig, pend, count):
     """First ``count`` samples of GLOBAL channel 0 after ``pend`` (without
-    noise), on any shard: replayed from the source when it is generated,
-    else read from the local buffer or the channel-0 shadow."""
+    noise), on any shard: replayed for global channels 0..1 (the pairing the
+    full run uses, so the values are bit-identical to the final channel 0)
+    from the source when it is generated, else from the local buffer or the
+    channel-0 shadow."""
     N = sig._ncols
-    base = None
+    nrow = min(2, sig.Nchan)
+    scratch = torch.empty((nrow, N), dtype=torch.float32, device=device())
     if pend.source is None:
-        base = sig._buf[0:1] if sig._c0 == 0 else sig._row0
+        if sig._c0 == 0 and sig._c1 >= nrow:
+            base = sig._buf[0:nrow]
+        else:
+            base = sig._row0
         if base is None:
             raise RuntimeError("no data for channel 0")
-    scratch = torch.empty((1, N), dtype=torch.float32, device=device())
-    if base is not None:
         scratch.copy_(base)
     probe = Pending(pend.source)
     probe.shifts = list(pend.shifts)
     probe.null = pend.null
-    if probe.empty():
-        return scratch[0, :count].cpu().numpy()
-    p, keep = build_pipeline(sig, probe, 1, 0, scratch)
-    run(p, keep)
+    if not probe.empty():
+        p, keep = build_pipeline(sig, probe, nrow, 0, scratch)
+        run(p, keep)
     return scratch[0, :count].cpu().numpy().astype(np.float64)

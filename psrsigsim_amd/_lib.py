@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpss_hip.so")
+LIB_PATH = os.environ.get("PSS_LIB_PATH") or os.path.join(_HERE, "libpss_hip.so")
 
 PSS_OK, PSS_EINVAL, PSS_EUNSUPPORTED, PSS_EHIP = 0, -1, -2, -3
 SRC_LOAD, SRC_SEARCH, SRC_FOLD = 0, 1, 2

@@ -18,7 +18,13 @@ __device__ __forceinline__ cf csub(cf a, cf b) { return make_float2(a.x - b.x, a
 // v_cos_f32 (input in revolutions; measured max abs error 1.2e-7 on MI355X,
 // tools/probe_trig.hip).  |r| <= 0.5 keeps the argument's own rounding small.
 __device__ __forceinline__ cf expi_rev(float r) {
+#ifdef PSS_ACCURATE_TRIG
+    float s, c;
+    sincospif(2.0f * r, &s, &c);
+    return make_float2(c, s);
+#else
     return make_float2(__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r));
+#endif
 }
 
 // 2^-64-cycle fixed point phase -> signed revolutions in [-0.5, 0.5).

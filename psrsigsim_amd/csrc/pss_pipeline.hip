@@ -85,6 +85,12 @@ struct KP {
     int64_t N1;     // four-step: column length (1 for single-pass)
     int64_t N2;     // four-step: row length    (N for single-pass)
     float invN;
+    // four-step pair mode (two channels per complex row)
+    int npairs;
+    int poff;       // chan0 & 1: pairs are (even, odd) GLOBAL channels
+    cf *Yd;         // data pair spill    [npairs][N1][N2]
+    cf *Ym;         // mask pair spill    [npairs][N1][N2]
+    const cf *Mspec;// mask spectrum      [N1][N2] (natural k2 per row k1)
 };
 
 __device__ __forceinline__ int64_t floordiv(int64_t a, int64_t b) {
@@ -152,7 +158,8 @@ __device__ __forceinline__ float pchip_eval(const KP &k, int prow, int64_t n) {
 // re = data (generated or loaded, with an undelayed null applied);
 // im = delayed-null box mask (0 elsewhere).
 __device__ __forceinline__ void source4(const KP &k, int r, int64_t n0, int cnt,
-                                        float (&re)[4], float (&im)[4], bool want_re) {
+                                        float (&re)[4], float (&im)[4], bool want_re,
+                                        bool want_im = true) {
     const PssPipeline &p = k.p;
     const uint32_t c = (uint32_t)(p.chan0 + r);
 #pragma unroll
@@ -195,7 +202,7 @@ __device__ __forceinline__ void source4(const KP &k, int r, int64_t n0, int cnt,
             }
         }
     }
-    if (p.null_mode == PSS_NULL_DELAYED) {
+    if (want_im && p.null_mode == PSS_NULL_DELAYED) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             int rk, j;
@@ -492,11 +499,11 @@ __global__ __launch_bounds__(T) void k_colA(KP k) { C::passA(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_colC(KP k) { C::passC(k); }
 
-template <int N2, int BR, int T, typename FWD, typename INV>
+template <int N2, int BR, int T, typename FWD, typename INV, bool FWD_ONLY = false>
 struct Rows;
 
-template <int N2, int BR, int T, int... F, int... I>
-struct Rows<N2, BR, T, RList<F...>, RList<I...>> {
+template <int N2, int BR, int T, int... F, int... I, bool FWD_ONLY>
+struct Rows<N2, BR, T, RList<F...>, RList<I...>, FWD_ONLY> {
     using FF = Fft<N2, BR, T>;
     static constexpr int E = FF::E;
     static constexpr int RF0 = FF::template first<F...>();
@@ -519,6 +526,16 @@ struct Rows<N2, BR, T, RList<F...>, RList<I...>> {
             for (int q = 0; q < RF0; ++q) v[ib * RF0 + q] = Y[(int64_t)b * N2 + jj + q * LR];
         }
         FF::template run<false, 1, F...>(v, lds, tid);
+        if constexpr (FWD_ONLY) {
+            // spectrum in natural k2 order per row k1 (mask spectrum for pair mode)
+#pragma unroll
+            for (int i = 0; i < E; ++i) {
+                int b, k2;
+                FF::template where<RFL>(i, tid, b, k2);
+                Y[(int64_t)b * N2 + k2] = v[i];
+            }
+            return;
+        }
         const int64_t N1 = k.N1;
 #pragma unroll
         for (int i = 0; i < E; ++i) {
@@ -539,6 +556,267 @@ struct Rows<N2, BR, T, RList<F...>, RList<I...>> {
 
 template <typename R, int T>
 __global__ __launch_bounds__(T) void k_row(KP k) { R::pass(k); }
+
+// ---------------------------------------------------------------------------
+// path 2b: four-step in PAIR mode.  Two channels a = 2p, b = 2p+1 share one
+// complex row z = d_a + i d_b (half the spill bytes and half the column FFTs).
+// The row pass separates their spectra with the Hermitian pairing
+//   D_a(k) = (Z(k) + conj Z(N-k)) / 2,   D_b(k) = (Z(k) - conj Z(N-k)) / 2i,
+// bin N-k of row k1 living in row N1-k1 (column N2-1-k2; row 0 and N1/2 pair
+// with themselves), applies each channel's ramp and recombines
+// W = D_a R_a + i D_b R_b before the inverse.  A delayed-null mask (same row
+// for every channel) is transformed once per run (Mspec) and turned into the
+// pair V = M R'_a + i M R'_b by the row pass, spilled, and inverted by pass C
+// next to the data.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ cf ramp_rot(const KP &k, int r, int64_t kb) {
+    const int64_t kk = (2 * kb > k.N) ? kb - k.N : kb;
+    const uint64_t ph = (uint64_t)kk * k.p.ramp[r];
+    return expi_rev(-fix_to_rev(ph));
+}
+
+// W(k) from Z(k), Zm = Z(N-k) for channels ra, rb
+__device__ __forceinline__ cf pair_ramp(const KP &k, int ra, int rb, int64_t kb, cf Z, cf Zm) {
+    const cf Da = make_float2(0.5f * (Z.x + Zm.x), 0.5f * (Z.y - Zm.y));
+    const cf Db = make_float2(0.5f * (Z.y + Zm.y), 0.5f * (Zm.x - Z.x));
+    if (2 * kb == k.N) return make_float2(Da.x * k.p.nyq_re[ra], Db.x * k.p.nyq_re[rb]);
+    if (kb == 0) return make_float2(Da.x - Db.y, Da.y + Db.x);
+    const cf A = cmul(Da, ramp_rot(k, ra, kb));
+    const cf Bv = cmul(Db, ramp_rot(k, rb, kb));
+    return make_float2(A.x - Bv.y, A.y + Bv.x);
+}
+
+// V(k) = M(k) R'_a + i M(k) R'_b (mask Nyquist factor nyq_im)
+__device__ __forceinline__ cf mask_ramp(const KP &k, int ra, int rb, int64_t kb, cf M) {
+    if (2 * kb == k.N) return make_float2(M.x * k.p.nyq_im[ra], M.x * k.p.nyq_im[rb]);
+    if (kb == 0) return make_float2(M.x - M.y, M.y + M.x);
+    const cf A = cmul(M, ramp_rot(k, ra, kb));
+    const cf Bv = cmul(M, ramp_rot(k, rb, kb));
+    return make_float2(A.x - Bv.y, A.y + Bv.x);
+}
+
+template <int N2, int T, typename FWD, typename INV>
+struct PairRows;
+
+template <int N2, int T, int... F, int... I>
+struct PairRows<N2, T, RList<F...>, RList<I...>> {
+    using FF = Fft<N2, 2, T>;
+    static constexpr int E = FF::E;
+    static constexpr int RF0 = FF::template first<F...>();
+    static constexpr int RFL = FF::template last_of<F...>();
+    static constexpr int RIL = FF::template last_of<I...>();
+    static_assert(RIL == RF0, "inverse plan must be the reversed forward plan");
+    static constexpr int LR = N2 / RF0;
+
+    __device__ static void pass(const KP &k) {
+        __shared__ cf lds[2 * Lds<N2>::RS];
+        const int tid = threadIdx.x;
+        const int pr = blockIdx.x;                 // channel pair
+        const int j = blockIdx.y;                  // row pair {j, N1-j}; {0, N1/2}
+        const int N1 = (int)k.N1;
+        const int rowA = j, rowB = (j == 0) ? N1 / 2 : N1 - j;
+        const int ra = max(2 * pr - k.poff, 0), rb = min(2 * pr + 1 - k.poff, k.p.nchan - 1);
+        const bool data = k.p.data_in_fft != 0;
+        const bool mask = k.p.null_mode == PSS_NULL_DELAYED;
+        cf v[E];
+        if (data) {
+            cf *Y = k.Yd + (int64_t)pr * k.N;
+#pragma unroll
+            for (int ib = 0; ib < E / RF0; ++ib) {
+                const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
+                const cf *src = Y + (int64_t)(b ? rowB : rowA) * N2 + jj;
+#pragma unroll
+                for (int q = 0; q < RF0; ++q) v[ib * RF0 + q] = src[q * LR];
+            }
+            FF::template run<false, 1, F...>(v, lds, tid);
+            FF::template store<RFL>(v, lds, tid);
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < E; ++i) {
+                int b, k2;
+                FF::template where<RFL>(i, tid, b, k2);
+                const int row = b ? rowB : rowA;
+                int bm, k2m;
+                if (j == 0) { bm = b; k2m = (row == 0) ? ((N2 - k2) & (N2 - 1)) : (N2 - 1 - k2); }
+                else        { bm = 1 - b; k2m = N2 - 1 - k2; }
+                const cf Zm = lds[Lds<N2>::at(bm, k2m)];
+                v[i] = pair_ramp(k, ra, rb, row + (int64_t)N1 * k2, v[i], Zm);
+            }
+            __syncthreads();
+            FF::template run<true, 1, I...>(v, lds, tid);
+#pragma unroll
+            for (int ib = 0; ib < E / RF0; ++ib) {
+                const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
+                cf *dst = Y + (int64_t)(b ? rowB : rowA) * N2 + jj;
+#pragma unroll
+                for (int q = 0; q < RF0; ++q) dst[q * LR] = v[ib * RF0 + q];
+            }
+        }
+        if (mask) {
+            cf *V = k.Ym + (int64_t)pr * k.N;
+#pragma unroll
+            for (int i = 0; i < E; ++i) {
+                int b, k2;
+                FF::template where<RFL>(i, tid, b, k2);
+                const int row = b ? rowB : rowA;
+                const cf M = k.Mspec[(int64_t)row * N2 + k2];
+                v[i] = mask_ramp(k, ra, rb, row + (int64_t)N1 * k2, M);
+            }
+            __syncthreads();
+            FF::template run<true, 1, I...>(v, lds, tid);
+#pragma unroll
+            for (int ib = 0; ib < E / RF0; ++ib) {
+                const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
+                cf *dst = V + (int64_t)(b ? rowB : rowA) * N2 + jj;
+#pragma unroll
+                for (int q = 0; q < RF0; ++q) dst[q * LR] = v[ib * RF0 + q];
+            }
+        }
+    }
+};
+
+template <typename R, int T>
+__global__ __launch_bounds__(T) void k_pair_row(KP k) { R::pass(k); }
+
+template <int N1, int B, int T, typename FWD, typename INV>
+struct PairCols;
+
+template <int N1, int B, int T, int... F, int... I>
+struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
+    using FF = Fft<N1, B, T>;
+    static constexpr int E = FF::E;
+    static constexpr int RF0 = FF::template first<F...>();
+    static constexpr int RFL = FF::template last_of<F...>();
+    static constexpr int RI0 = FF::template first<I...>();
+    static constexpr int RIL = FF::template last_of<I...>();
+    static constexpr int ITEMS = N1 * B / 4 / T;
+    static_assert(ITEMS * 4 * T == N1 * B, "items per thread");
+
+    // A: generate channels a, b into z = d_a + i d_b; column FFTs; twiddle; spill
+    __device__ static void passA(const KP &k) {
+        __shared__ cf lds[B * Lds<N1>::RS];
+        const int tid = threadIdx.x;
+        const int pr = blockIdx.y;
+        const int ra = 2 * pr - k.poff, rb = ra + 1;
+        const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
+        const int64_t n20 = (int64_t)blockIdx.x * B;
+        const int64_t N2 = k.N2;
+        for (int it = tid; it < N1 * B / 4; it += T) {
+            const int n1 = it / (B / 4);
+            const int b4 = (it - n1 * (B / 4)) * 4;
+            const int64_t n = n1 * N2 + n20 + b4;
+            float xa[4], xb[4], dum[4];
+            if (hasa) source4(k, ra, n, 4, xa, dum, true, false);
+            else { xa[0] = xa[1] = xa[2] = xa[3] = 0.f; }
+            if (hasb) source4(k, rb, n, 4, xb, dum, true, false);
+            else { xb[0] = xb[1] = xb[2] = xb[3] = 0.f; }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lds[Lds<N1>::at(b4 + i, n1)] = make_float2(xa[i], xb[i]);
+        }
+        __syncthreads();
+        cf v[E];
+        FF::template load<RF0>(v, lds, tid);
+        __syncthreads();
+        FF::template run<false, 1, F...>(v, lds, tid);
+        const float invN = k.invN;
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+            int b, k1;
+            FF::template where<RFL>(i, tid, b, k1);
+            const int64_t m = (n20 + b) * (int64_t)k1;
+            float rev = (float)m * invN;
+            if (rev >= 0.5f) rev -= 1.0f;
+            v[i] = cmul(v[i], expi_rev(-rev));
+        }
+        FF::template store<RFL>(v, lds, tid);
+        __syncthreads();
+        cf *Y = k.Yd + (int64_t)pr * k.N;
+        for (int it = tid; it < N1 * B / 4; it += T) {
+            const int k1 = it / (B / 4);
+            const int b4 = (it - k1 * (B / 4)) * 4;
+            cf a0 = lds[Lds<N1>::at(b4 + 0, k1)], a1 = lds[Lds<N1>::at(b4 + 1, k1)];
+            cf a2 = lds[Lds<N1>::at(b4 + 2, k1)], a3 = lds[Lds<N1>::at(b4 + 3, k1)];
+            float4 *dst = reinterpret_cast<float4 *>(Y + (int64_t)k1 * N2 + n20 + b4);
+            dst[0] = make_float4(a0.x, a0.y, a1.x, a1.y);
+            dst[1] = make_float4(a2.x, a2.y, a3.x, a3.y);
+        }
+    }
+
+    // inverse column FFTs of one spilled pair block into (re, im) per item
+    __device__ static void inv_block(const KP &k, const cf *Yp, int64_t n20, cf *lds, int tid,
+                                     float (&re)[ITEMS][4], float (&im)[ITEMS][4]) {
+        const int64_t N2 = k.N2;
+        const float invN = k.invN;
+        for (int it = tid; it < N1 * B / 4; it += T) {
+            const int k1 = it / (B / 4);
+            const int b4 = (it - k1 * (B / 4)) * 4;
+            const float4 *src = reinterpret_cast<const float4 *>(Yp + (int64_t)k1 * N2 + n20 + b4);
+            const float4 lo = src[0], hi = src[1];
+            const cf a[4] = {make_float2(lo.x, lo.y), make_float2(lo.z, lo.w),
+                             make_float2(hi.x, hi.y), make_float2(hi.z, hi.w)};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t m = (n20 + b4 + i) * (int64_t)k1;
+                float rev = (float)m * invN;
+                if (rev >= 0.5f) rev -= 1.0f;
+                lds[Lds<N1>::at(b4 + i, k1)] = cmul(a[i], expi_rev(rev));
+            }
+        }
+        __syncthreads();
+        cf v[E];
+        FF::template load<RI0>(v, lds, tid);
+        __syncthreads();
+        FF::template run<true, 1, I...>(v, lds, tid);
+        FF::template store<RIL>(v, lds, tid);
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < ITEMS; ++t) {
+            const int it = tid + t * T;
+            const int n1 = it / (B / 4);
+            const int b4 = (it - n1 * (B / 4)) * 4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const cf z = lds[Lds<N1>::at(b4 + i, n1)];
+                re[t][i] = z.x * invN;
+                im[t][i] = z.y * invN;
+            }
+        }
+        __syncthreads();
+    }
+
+    // C: inverse column FFTs of the data pair (and mask pair), epilogues of a, b
+    __device__ static void passC(const KP &k) {
+        __shared__ cf lds[B * Lds<N1>::RS];
+        const int tid = threadIdx.x;
+        const int pr = blockIdx.y;
+        const int ra = 2 * pr - k.poff, rb = ra + 1;
+        const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
+        const int64_t n20 = (int64_t)blockIdx.x * B;
+        const bool data = k.p.data_in_fft != 0;
+        const bool mask = k.p.null_mode == PSS_NULL_DELAYED;
+        float da[ITEMS][4], db[ITEMS][4], ma[ITEMS][4], mb[ITEMS][4];
+#pragma unroll
+        for (int t = 0; t < ITEMS; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { da[t][i] = db[t][i] = ma[t][i] = mb[t][i] = 0.f; }
+        if (data) inv_block(k, k.Yd + (int64_t)pr * k.N, n20, lds, tid, da, db);
+        if (mask) inv_block(k, k.Ym + (int64_t)pr * k.N, n20, lds, tid, ma, mb);
+#pragma unroll
+        for (int t = 0; t < ITEMS; ++t) {
+            const int it = tid + t * T;
+            const int n1 = it / (B / 4);
+            const int b4 = (it - n1 * (B / 4)) * 4;
+            const int64_t n = n1 * k.N2 + n20 + b4;
+            if (hasa) epilogue4(k, ra, n, 4, da[t], ma[t], !data);
+            if (hasb) epilogue4(k, rb, n, 4, db[t], mb[t], !data);
+        }
+    }
+};
+
+template <typename C, int T>
+__global__ __launch_bounds__(T) void k_pairA(KP k) { C::passA(k); }
+template <typename C, int T>
+__global__ __launch_bounds__(T) void k_pairC(KP k) { C::passC(k); }
 
 // ---------------------------------------------------------------------------
 // path 3: direct DFT fallback for even N that are not handled above.
@@ -716,27 +994,6 @@ static int launch_single(const KP &k, hipStream_t st) {
     return PSS_OK;
 }
 
-template <int N1, int B, int T, typename CF, typename CI, int N2, int BR, int TR, typename RF, typename RI>
-static int launch_four(const KP &k, hipStream_t st) {
-    using C = Cols<N1, B, T, CF, CI>;
-    using R = Rows<N2, BR, TR, RF, RI>;
-    dim3 gc((unsigned)(N2 / B), (unsigned)k.p.nchan);
-    tk_begin(TK_COLA, st);
-    k_colA<C, T><<<gc, dim3(T), 0, st>>>(k);
-    tk_end(st);
-    LAUNCHCHK();
-    dim3 gr((unsigned)(N1 / BR), (unsigned)k.p.nchan);
-    tk_begin(TK_ROW, st);
-    k_row<R, TR><<<gr, dim3(TR), 0, st>>>(k);
-    tk_end(st);
-    LAUNCHCHK();
-    tk_begin(TK_COLC, st);
-    k_colC<C, T><<<gc, dim3(T), 0, st>>>(k);
-    tk_end(st);
-    LAUNCHCHK();
-    return PSS_OK;
-}
-
 // Column plans: B*N1 = 8192 complex per workgroup, 512 threads, 16 per thread.
 // Row plans: N2 = 8192 (1 row, 512 thr) or N2 <= 4096 (4096/N2 rows, 256 thr).
 using C16 = RList<16>;
@@ -757,15 +1014,63 @@ using C4k = RList<16, 16, 16>;
 using C8kF = RList<16, 16, 16, 2>;
 using C8kI = RList<2, 16, 16, 16>;
 
-static int run_fourstep(KP &k, hipStream_t st) {
+template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typename RF, typename RI,
+          int TRF>
+static int launch_pair(KP &k, hipStream_t st, float *mask_row) {
+    using PC = PairCols<N1, B, T, CF, CI>;
+    using PR = PairRows<N2, TR, RF, RI>;
+    k.poff = k.p.chan0 & 1;
+    k.npairs = (k.p.nchan + k.poff + 1) / 2;
+    char *w = reinterpret_cast<char *>(k.p.work);
+    k.Yd = reinterpret_cast<cf *>(w);
+    k.Ym = reinterpret_cast<cf *>(w + (int64_t)k.npairs * k.N * 8);
+    cf *mspec = reinterpret_cast<cf *>(w + (int64_t)2 * k.npairs * k.N * 8);
+    k.Mspec = mspec;
+    if (k.p.null_mode == PSS_NULL_DELAYED) {
+        // spectrum of the (channel independent) mask row, once per run
+        KP km = k;
+        km.p.nchan = 1;
+        km.p.chan0 = 0;
+        km.p.data = mask_row;
+        km.p.ld = k.N;
+        km.p.src = PSS_SRC_LOAD;
+        km.p.null_mode = PSS_NULL_NONE;
+        km.p.data_in_fft = 1;
+        km.p.work = mspec;
+        using C1 = Cols<N1, B, T, CF, CI>;
+        using R1 = Rows<N2, 1, TRF, RF, RI, true>;
+        k_colA<C1, T><<<dim3((unsigned)(N2 / B), 1), dim3(T), 0, st>>>(km);
+        LAUNCHCHK();
+        k_row<R1, TRF><<<dim3((unsigned)N1, 1), dim3(TRF), 0, st>>>(km);
+        LAUNCHCHK();
+    }
+    dim3 gc((unsigned)(N2 / B), (unsigned)k.npairs);
+    if (k.p.data_in_fft) {
+        tk_begin(TK_COLA, st);
+        k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
+        tk_end(st);
+        LAUNCHCHK();
+    }
+    tk_begin(TK_ROW, st);
+    k_pair_row<PR, TR><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
+    tk_end(st);
+    LAUNCHCHK();
+    tk_begin(TK_COLC, st);
+    k_pairC<PC, T><<<gc, dim3(T), 0, st>>>(k);
+    tk_end(st);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+static int run_fourstep(KP &k, hipStream_t st, float *mask_row) {
     const int64_t N = k.N;
     if (N >= (1 << 17)) {
         k.N2 = 8192;
         k.N1 = N / 8192;
         switch (k.N1) {
-#define CASE8K(N1_, CF, CI)                                                                      \
-    case N1_:                                                                                    \
-        return launch_four<N1_, 8192 / N1_, 512, CF, CI, 8192, 1, 512, C8kF, C8kI>(k, st);
+#define CASE8K(N1_, CF, CI)                                                                          \
+    case N1_:                                                                                        \
+        return launch_pair<N1_, 8192 / N1_, 512, CF, CI, 8192, 1024, C8kF, C8kI, 512>(k, st, mask_row);
             CASE8K(16, C16, C16)
             CASE8K(32, C32F, C32I)
             CASE8K(64, C64F, C64I)
@@ -784,11 +1089,11 @@ static int run_fourstep(KP &k, hipStream_t st) {
     k.N2 = N / 16;
     switch (k.N2) {
         case 1024:
-            return launch_four<16, 512, 512, C16, C16, 1024, 4, 256, C1kF, C1kI>(k, st);
+            return launch_pair<16, 512, 512, C16, C16, 1024, 128, C1kF, C1kI, 64>(k, st, mask_row);
         case 2048:
-            return launch_four<16, 512, 512, C16, C16, 2048, 2, 256, C2kF, C2kI>(k, st);
+            return launch_pair<16, 512, 512, C16, C16, 2048, 256, C2kF, C2kI, 128>(k, st, mask_row);
         case 4096:
-            return launch_four<16, 512, 512, C16, C16, 4096, 1, 256, C4k, C4k>(k, st);
+            return launch_pair<16, 512, 512, C16, C16, 4096, 512, C4k, C4k, 256>(k, st, mask_row);
         default: break;
     }
     return fail(PSS_EUNSUPPORTED, "four-step: N=%lld", (long long)N);
@@ -891,7 +1196,9 @@ int pss_last_error(char *buf, size_t n) {
 // Layout: [spill area][mask row: nsamp floats, 256-B aligned]
 static int64_t spill_bytes(int32_t nchan, int64_t nsamp) {
     const int64_t one = (int64_t)nchan * nsamp * 8;
-    if (is_pow2(nsamp) && nsamp >= 64 && nsamp <= (1ll << 24)) return nsamp > 8192 ? one : 0;
+    const int64_t npairs = (nchan + 2) / 2;   // pairs of (even, odd) global channels
+    if (is_pow2(nsamp) && nsamp >= 64 && nsamp <= (1ll << 24))
+        return nsamp > 8192 ? 2 * npairs * nsamp * 8 + nsamp * 8 : 0;   // Yd, Ym, Mspec
     return 2 * one + nsamp * 8;   // fallback: W1, W2 and the twiddle table
 }
 
@@ -919,15 +1226,19 @@ int pss_run(const PssPipeline *p, void *stream) {
         return PSS_OK;
     }
     const int64_t N = p->nsamp;
-    if (p->null_mode == PSS_NULL_DELAYED && !p->inj_box) {
-        float *row = reinterpret_cast<float *>(reinterpret_cast<char *>(p->work) +
-                                               ((spill_bytes(p->nchan, N) + 255) & ~255ll));
-        k_box_row<<<stream_grid(N, 1), dim3(256), 0, st>>>(k, row);
-        LAUNCHCHK();
-        k.p.inj_box = row;
+    float *row = reinterpret_cast<float *>(reinterpret_cast<char *>(p->work) +
+                                           ((spill_bytes(p->nchan, N) + 255) & ~255ll));
+    if (p->null_mode == PSS_NULL_DELAYED) {
+        if (!p->inj_box) {
+            k_box_row<<<stream_grid(N, 1), dim3(256), 0, st>>>(k, row);
+            LAUNCHCHK();
+            k.p.inj_box = row;
+        } else {
+            row = const_cast<float *>(p->inj_box);
+        }
     }
     if (is_pow2(N) && N >= 64 && N <= 8192) return run_single(k, st);
-    if (is_pow2(N) && N >= 16384 && N <= (1ll << 24)) return run_fourstep(k, st);
+    if (is_pow2(N) && N >= 16384 && N <= (1ll << 24)) return run_fourstep(k, st, row);
     return run_fallback(k, st);
 }
 

@@ -7,6 +7,7 @@ delay stages run as ONE forward/inverse FFT pass on the GPU (the reference runs
 one rfft/irfft pair per channel per call: ism.py:57-60, 136-139, 203-206).
 """
 import numpy as np
+from scipy.signal import fftconvolve as _fftconvolve
 
 from ..utils.constants import DM_K_VALUE, KOLMOGOROV_BETA
 from ..utils.utils import make_quant
@@ -108,9 +109,10 @@ class ISM(object):
         pn = np.where(ps != 0.0, prof[:rows] / np.where(ps != 0.0, ps, 1.0), prof[:rows])
         ks = np.sum(kern, axis=1, keepdims=True)
         kn = np.where(ks != 0.0, kern / np.where(ks != 0.0, ks, 1.0), kern)
-        n = pn.shape[1] + kn.shape[1] - 1
-        nfft = 1 << int(np.ceil(np.log2(n)))           # linear convolution, zero padded
-        conv = np.fft.irfft(np.fft.rfft(pn, nfft, axis=1) * np.fft.rfft(kn, nfft, axis=1), nfft, axis=1)
+        # scipy's FFT convolution batched over rows: bit-identical to the
+        # reference's per-row scipy.signal.convolve(..., method='fft') (the
+        # reference later makes exact float decisions on these values).
+        conv = _fftconvolve(pn, kn, mode='full', axes=1)
         profiles[:rows, :] = ps * conv[:, :width]
         return profiles
 

@@ -77,21 +77,28 @@ def pchip_coefficients(x, y):
 
 def ppoly_eval(x, c, ph, y=None):
     """Evaluate the piecewise cubic at phases ``ph`` (extrapolating with the
-    end pieces); returns [rows, len(ph)].  Phases that are exactly the first
-    len(ph) knots return the knot values ``y`` (t = 0 exactly)."""
+    end pieces); returns [rows, len(ph)].
+
+    The arithmetic replicates the published PPoly evaluation scipy performs for
+    the reference (power accumulation res += c_k * s^k, s^k by repeated
+    multiplication, lowest power first; interval = last breakpoint <= x,
+    clipped to the end pieces) bit for bit, because the reference makes exact
+    float decisions on these values (the periodic-closure test at
+    portraits.py:234 compares generator(0) with generator(1))."""
     ph = np.asarray(ph, dtype=float)
     if y is not None and ph.size <= x.size and np.array_equal(ph, x[:ph.size]):
         return np.array(y[:, :ph.size])
     i = np.clip(np.searchsorted(x, ph, side="right") - 1, 0, x.size - 2)
-    t = (ph - x[i])[None, :]
+    s = (ph - x[i])[None, :]
     ci = c[:, i, :]
-    out = ci[:, :, 0] * t
-    out += ci[:, :, 1]
-    out *= t
-    out += ci[:, :, 2]
-    out *= t
-    out += ci[:, :, 3]
-    return out
+    res = ci[:, :, 3] * 1.0
+    z = s
+    res = res + ci[:, :, 2] * z
+    z = z * s
+    res = res + ci[:, :, 1] * z
+    z = z * s
+    res = res + ci[:, :, 0] * z
+    return res
 
 
 # ---------------------------------------------------------------------------

@@ -34,7 +34,9 @@ def test_workspace_sizes():
     L = _lib.load()
     # [spill area, 256-B aligned][null mask row: nsamp floats]
     assert L.pss_workspace_bytes(4, 4096) == 4096 * 4               # single pass: LDS only
-    assert L.pss_workspace_bytes(4, 1 << 20) == 4 * (1 << 20) * 8 + (1 << 20) * 4
+    n = 1 << 20          # pair mode: Yd + Ym ((nchan+2)//2 pairs, parity-aligned) + Mspec + mask row
+    assert L.pss_workspace_bytes(4, n) == 2 * 3 * n * 8 + n * 8 + n * 4
+    assert L.pss_workspace_bytes(3, n) == 2 * 2 * n * 8 + n * 8 + n * 4
     sp = 2 * 2 * 244 * 8 + 244 * 8                                   # fallback W1, W2, twiddles
     assert L.pss_workspace_bytes(2, 244) == ((sp + 255) // 256) * 256 + 244 * 4
 

@@ -71,3 +71,27 @@ def test_odd_length_disperse_raises(hip_lib):
     assert sig.nsamp % 2 == 1
     with pytest.raises(ValueError):
         ISM().disperse(sig, 10)
+
+
+def _big_case(log2n, nchan, null=True, fd=True):
+    ops = [("scatter_conv", 1e-4, 1400, None), ("make_pulses", (1 << log2n) * 20.48e-6, "pulses"),
+           ("disperse", 100, "disperse")]
+    if fd:
+        ops.append(("fd", [2e-4, -3e-5], "fd"))
+    if null:
+        ops.append(("null", 0.1, "null"))
+    ops.append(("observe", "Arecibo", "Lband_PUPPI", True, "noise"))
+    return dict(sig=dict(fcent=1400, bw=400, nchan=nchan, fold=False),
+                psr=dict(period=0.005, Smean=1.0, prof=("gauss", 0.5, 0.05, 1)), ops=ops)
+
+
+@pytest.mark.parametrize("fused", [True, False], ids=["fused", "staged"])
+@pytest.mark.parametrize("log2n,nchan,null", [(14, 3, True), (16, 3, True), (17, 2, True),
+                                               (17, 3, False), (20, 1, True)])
+def test_fourstep_pair_path_vs_oracle(log2n, nchan, null, fused, hip_lib):
+    """The four-step PAIR path (odd and even channel counts, with and without
+    the delayed-null mask, fused and staged = mask-only FFT) against the
+    oracle run with legacy RandomState draws, injected into the GPU run."""
+    errs = replay.run_case(None, fused=fused, case=_big_case(log2n, nchan, null=null), seed=log2n)
+    bad = {k: v for k, v in errs.items() if not v <= TOL}
+    assert not bad, errs

@@ -168,3 +168,24 @@ def test_pchip_matches_scipy():
     P = PchipInterpolator(x, y, axis=1)
     ph = np.linspace(-0.01, 1.02, 2000)
     np.testing.assert_allclose(ppoly_eval(x, c, ph), P(ph), rtol=0, atol=1e-13)
+
+
+@pytest.mark.parametrize("nchan", [1, 2, 3, 8, 64])
+def test_scatter_convolution_bitwise_vs_reference_structure(nchan):
+    """The batched host convolution equals the reference's per-row
+    scipy.signal.convolve(method='fft') (via the oracle) bit for bit, and so
+    does the periodic-closure decision that depends on it (portraits.py:234)."""
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+    from psrsigsim_amd.ism import ISM
+    sig = FilterBankSignal(1400, 400, Nsubband=nchan, fold=False)
+    psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
+    ISM().scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
+    osig = O.Signal(1400, 400, nchan=nchan, fold=False)
+    opsr = O.Pulsar(0.005, 1.0, profiles=O.GaussPortrait(0.5, 0.05, 1))
+    O.scatter_broaden(osig, 1e-4, 1400, convolve=True, pulsar=opsr)
+    np.testing.assert_array_equal(psr.Profiles._kvals, opsr.Profiles.knot_y)
+    psr.make_pulses(sig, (1 << 16) * 20.48e-6)
+    opsr.ref_freq = 1400.0
+    O.add_spec_idx(osig, opsr)
+    assert sig._pending.source.nint == opsr.Profiles.knot_x.size - 1
