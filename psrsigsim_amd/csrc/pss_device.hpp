@@ -34,14 +34,39 @@ __device__ __forceinline__ float fix_to_rev(uint64_t ph) {
 }
 
 // --------------------------------------------------------------------------
+// Buffer (SRD) access: 32-bit per-lane byte offsets plus a scalar offset, so a
+// run of strided accesses costs no per-access 64-bit address VGPRs.  The base
+// must be wave-uniform (kernel arguments / blockIdx only).
+// --------------------------------------------------------------------------
+struct Buf {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ __forceinline__ Buf(const void *base, uint32_t bytes)
+        : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, bytes, 0x00020000)) {}
+    __device__ __forceinline__ cf ld2(uint32_t voff, uint32_t soff) const {
+        typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+        u2 w = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+        return make_float2(__uint_as_float(w.x), __uint_as_float(w.y));
+    }
+    __device__ __forceinline__ void st2(cf v, uint32_t voff, uint32_t soff) const {
+        typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+        u2 w;
+        w.x = __float_as_uint(v.x);
+        w.y = __float_as_uint(v.y);
+        __builtin_amdgcn_raw_buffer_store_b64(w, r, voff, soff, 0);
+    }
+};
+
+// --------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11)
 // --------------------------------------------------------------------------
 __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-        uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
-        c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+        // one v_mad_u64_u32 per product (hi and lo together), not mul_hi + mul_lo
+        const uint64_t p0 = (uint64_t)c.x * 0xD2511F53u;
+        const uint64_t p1 = (uint64_t)c.z * 0xCD9E8D57u;
+        c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1,
+                       (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0);
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }

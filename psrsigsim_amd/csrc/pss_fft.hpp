@@ -140,14 +140,26 @@ struct Fft {
             const int k = jj % Ns;
             cf *a = v + ib * R;
             if constexpr (Ns > 1) {
-                // a[q] *= exp(-+2 pi i q k / (Ns R))   (exact rational angle)
+                // a[q] *= w^q, w = exp(-+2 pi i k / (Ns R)).  w^(2^j) from the
+                // native trig (angles < 1/2 rev), the other powers as products
+                // of at most four of those (<= 3 roundings).
+                constexpr int H = (R >= 8) ? R / 2 : R;   // powers kept: w^1 .. w^(H-1)
+                cf w[H];
+                const float base = (float)k * (1.0f / (float)(Ns * R));   // [0, 1/R)
 #pragma unroll
-                for (int q = 1; q < R; ++q) {
-                    int m = q * k;                       // < Ns*R <= L
-                    if (2 * m >= Ns * R) m -= Ns * R;    // [-1/2, 1/2) rev
-                    const float rev = (float)m * (1.0f / (float)(Ns * R));
-                    cf w = expi_rev(INV ? rev : -rev);
-                    a[q] = cmul(a[q], w);
+                for (int p2 = 1; p2 < H; p2 *= 2) w[p2] = expi_rev(INV ? p2 * base : -p2 * base);
+#pragma unroll
+                for (int q = 3; q < H; ++q) {
+                    const int hi = 1 << (31 - __builtin_clz(q));   // compile-time after unrolling
+                    if (q != hi) w[q] = cmul(w[hi], w[q - hi]);
+                }
+#pragma unroll
+                for (int q = 1; q < H; ++q) a[q] = cmul(a[q], w[q]);
+                if constexpr (H < R) {
+                    const cf wh = expi_rev(INV ? H * base : -H * base);
+                    a[H] = cmul(a[H], wh);
+#pragma unroll
+                    for (int q = 1; q < H; ++q) a[H + q] = cmul(a[H + q], cmul(wh, w[q]));
                 }
             }
             dft<R, INV>(a);

@@ -18,6 +18,13 @@
 #include "pss_fft.hpp"
 #include "../../include/pss_hip.h"
 
+// Diagnostic ablations (tools/ablate.sh): PSS_ABLATE bits switch parts of the
+// pair-mode kernels off to attribute their cost.  0 in every product build.
+#ifndef PSS_ABLATE
+#define PSS_ABLATE 0
+#endif
+static constexpr int kAbl = PSS_ABLATE;
+
 using namespace pss;
 
 // ---------------------------------------------------------------------------
@@ -142,12 +149,17 @@ __device__ __forceinline__ void draw4(const Rng &g, int64_t n0, uint32_t c, floa
 
 __device__ __forceinline__ float pchip_eval(const KP &k, int prow, int64_t n) {
     const PssPipeline &p = k.p;
-    const uint64_t ph = (uint64_t)n * p.phase_step;               // 2^-64 cycles
-    uint64_t iv = __umul64hi(ph, (uint64_t)p.knot_m);             // interval index
-    const uint64_t uf = ph * (uint64_t)p.knot_m;                   // fraction in it
-    float u = (float)(uf >> 40) * 5.9604644775390625e-08f;         // * 2^-24
-    if (iv >= (uint64_t)p.nint) {                                  // extrapolate
-        u += (float)(iv - (uint64_t)(p.nint - 1));
+    // ph = n * phase_step mod 2^64 (2^-64 cycles), n < 2^32: 32-bit products only
+    const uint32_t nn = (uint32_t)n;
+    const uint64_t ph = (uint64_t)nn * (uint32_t)p.phase_step +
+                        ((uint64_t)(nn * (uint32_t)(p.phase_step >> 32)) << 32);
+    // ph * M = iv 2^64 + fraction; u = (ph * M) >> 32 holds iv and fraction bits 32..63
+    const uint64_t t = (uint64_t)(uint32_t)ph * p.knot_m;
+    const uint64_t u64 = (uint64_t)(uint32_t)(ph >> 32) * p.knot_m + (t >> 32);
+    uint32_t iv = (uint32_t)(u64 >> 32);                           // interval index
+    float u = (float)((uint32_t)u64 >> 8) * 5.9604644775390625e-08f;   // fraction, 24 bits
+    if (iv >= (uint32_t)p.nint) {                                  // extrapolate
+        u += (float)(iv - (uint32_t)(p.nint - 1));
         iv = p.nint - 1;
     }
     const float4 cc = reinterpret_cast<const float4 *>(p.prof)[(int64_t)prow * p.nint + iv];
@@ -332,6 +344,7 @@ struct SinglePass<L, BATCH, T, RList<F...>, RList<I...>> {
     static constexpr int RF0 = FF::template first<F...>();
     static constexpr int RFL = FF::template last_of<F...>();
     static constexpr int RIL = FF::template last_of<I...>();
+    static_assert(RIL == RF0, "inverse plan must be the reversed forward plan");
 
     __device__ static void body(const KP &k) {
         __shared__ cf lds[BATCH * Lds<L>::RS];
@@ -569,30 +582,17 @@ __global__ __launch_bounds__(T) void k_row(KP k) { R::pass(k); }
 // pair V = M R'_a + i M R'_b by the row pass, spilled, and inverted by pass C
 // next to the data.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ cf ramp_rot(const KP &k, int r, int64_t kb) {
-    const int64_t kk = (2 * kb > k.N) ? kb - k.N : kb;
-    const uint64_t ph = (uint64_t)kk * k.p.ramp[r];
+// Ramps in the row pass.  A thread's last-stage (radix RFL) group holds bins
+// kb = kb0 + q N/RFL (q < RFL, kb0 < N/RFL); the reference's phase
+// kb' s / N (kb' = kb - N above N/2) is, in 64-bit fixed point,
+//   kb0 w + q (N/RFL) w - [2q >= RFL] N w   (mod 2^64, w = ramp word),
+// so per bin only a 64-bit add of a uniform (scalar) offset is needed --
+// bit-identical to multiplying kb' w directly.
+template <int RFL>
+__device__ __forceinline__ cf ramp_q(uint64_t p0, uint64_t step, uint64_t nw, int q) {
+    uint64_t ph = p0 + (uint64_t)q * step;
+    if (2 * q >= RFL) ph -= nw;                 // q is a compile-time constant here
     return expi_rev(-fix_to_rev(ph));
-}
-
-// W(k) from Z(k), Zm = Z(N-k) for channels ra, rb
-__device__ __forceinline__ cf pair_ramp(const KP &k, int ra, int rb, int64_t kb, cf Z, cf Zm) {
-    const cf Da = make_float2(0.5f * (Z.x + Zm.x), 0.5f * (Z.y - Zm.y));
-    const cf Db = make_float2(0.5f * (Z.y + Zm.y), 0.5f * (Zm.x - Z.x));
-    if (2 * kb == k.N) return make_float2(Da.x * k.p.nyq_re[ra], Db.x * k.p.nyq_re[rb]);
-    if (kb == 0) return make_float2(Da.x - Db.y, Da.y + Db.x);
-    const cf A = cmul(Da, ramp_rot(k, ra, kb));
-    const cf Bv = cmul(Db, ramp_rot(k, rb, kb));
-    return make_float2(A.x - Bv.y, A.y + Bv.x);
-}
-
-// V(k) = M(k) R'_a + i M(k) R'_b (mask Nyquist factor nyq_im)
-__device__ __forceinline__ cf mask_ramp(const KP &k, int ra, int rb, int64_t kb, cf M) {
-    if (2 * kb == k.N) return make_float2(M.x * k.p.nyq_im[ra], M.x * k.p.nyq_im[rb]);
-    if (kb == 0) return make_float2(M.x - M.y, M.y + M.x);
-    const cf A = cmul(M, ramp_rot(k, ra, kb));
-    const cf Bv = cmul(M, ramp_rot(k, rb, kb));
-    return make_float2(A.x - Bv.y, A.y + Bv.x);
 }
 
 template <int N2, int T, typename FWD, typename INV>
@@ -607,6 +607,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
     static constexpr int RIL = FF::template last_of<I...>();
     static_assert(RIL == RF0, "inverse plan must be the reversed forward plan");
     static constexpr int LR = N2 / RF0;
+    static constexpr int LRL = N2 / RFL;
 
     __device__ static void pass(const KP &k) {
         __shared__ cf lds[2 * Lds<N2>::RS];
@@ -618,58 +619,96 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
         const int ra = max(2 * pr - k.poff, 0), rb = min(2 * pr + 1 - k.poff, k.p.nchan - 1);
         const bool data = k.p.data_in_fft != 0;
         const bool mask = k.p.null_mode == PSS_NULL_DELAYED;
+        const uint64_t rwa = (uint64_t)k.p.ramp[ra], rwb = (uint64_t)k.p.ramp[rb];
+        // uniform 64-bit phase offsets of bin kb0 + q N/RFL relative to kb0 (SALU)
+        const uint64_t sta = (uint64_t)(k.N / RFL) * rwa, stb = (uint64_t)(k.N / RFL) * rwb;
+        const uint64_t nwa = (uint64_t)k.N * rwa, nwb = (uint64_t)k.N * rwb;
         cf v[E];
+        const uint32_t pbytes = (uint32_t)(k.N * 8);
         if (data) {
-            cf *Y = k.Yd + (int64_t)pr * k.N;
+            const Buf Y(k.Yd + (int64_t)pr * k.N, pbytes);
 #pragma unroll
             for (int ib = 0; ib < E / RF0; ++ib) {
                 const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
-                const cf *src = Y + (int64_t)(b ? rowB : rowA) * N2 + jj;
+                const uint32_t off = (uint32_t)((b ? rowB : rowA) * N2 + jj) * 8u;
 #pragma unroll
-                for (int q = 0; q < RF0; ++q) v[ib * RF0 + q] = src[q * LR];
+                for (int q = 0; q < RF0; ++q) v[ib * RF0 + q] = Y.ld2(off, q * LR * 8);
             }
-            FF::template run<false, 1, F...>(v, lds, tid);
+            if constexpr (!(kAbl & 2)) FF::template run<false, 1, F...>(v, lds, tid);
             FF::template store<RFL>(v, lds, tid);
             __syncthreads();
 #pragma unroll
-            for (int i = 0; i < E; ++i) {
-                int b, k2;
-                FF::template where<RFL>(i, tid, b, k2);
+            for (int ib = 0; ib < E / RFL; ++ib) {
+                const int jg = tid + ib * T, b = jg / LRL, jj = jg - b * LRL;
                 const int row = b ? rowB : rowA;
-                int bm, k2m;
-                if (j == 0) { bm = b; k2m = (row == 0) ? ((N2 - k2) & (N2 - 1)) : (N2 - 1 - k2); }
-                else        { bm = 1 - b; k2m = N2 - 1 - k2; }
-                const cf Zm = lds[Lds<N2>::at(bm, k2m)];
-                v[i] = pair_ramp(k, ra, rb, row + (int64_t)N1 * k2, v[i], Zm);
+                const int64_t kb0 = row + (int64_t)N1 * jj;
+                const uint64_t p0a = (uint64_t)kb0 * rwa, p0b = (uint64_t)kb0 * rwb;
+#pragma unroll
+                for (int q = 0; q < RFL; ++q) {
+                    const int i = ib * RFL + q, k2 = jj + q * LRL;
+                    int bm, k2m;
+                    if (j == 0) { bm = b; k2m = (row == 0) ? ((N2 - k2) & (N2 - 1)) : (N2 - 1 - k2); }
+                    else        { bm = 1 - b; k2m = N2 - 1 - k2; }
+                    const cf Z = v[i], Zm = lds[Lds<N2>::at(bm, k2m)];
+                    const cf Da = make_float2(0.5f * (Z.x + Zm.x), 0.5f * (Z.y - Zm.y));
+                    const cf Db = make_float2(0.5f * (Z.y + Zm.y), 0.5f * (Zm.x - Z.x));
+                    if constexpr (kAbl & 8) {
+                        v[i] = cadd(Da, Db);
+                    } else if (kb0 == 0 && 2 * q == RFL) {          // Nyquist bin
+                        v[i] = make_float2(Da.x * k.p.nyq_re[ra], Db.x * k.p.nyq_re[rb]);
+                    } else if (kb0 == 0 && q == 0) {                // DC
+                        v[i] = make_float2(Da.x - Db.y, Da.y + Db.x);
+                    } else {
+                        const cf A = cmul(Da, ramp_q<RFL>(p0a, sta, nwa, q));
+                        const cf Bv = cmul(Db, ramp_q<RFL>(p0b, stb, nwb, q));
+                        v[i] = make_float2(A.x - Bv.y, A.y + Bv.x);
+                    }
+                }
             }
             __syncthreads();
-            FF::template run<true, 1, I...>(v, lds, tid);
+            if constexpr (!(kAbl & 2)) FF::template run<true, 1, I...>(v, lds, tid);
 #pragma unroll
             for (int ib = 0; ib < E / RF0; ++ib) {
                 const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
-                cf *dst = Y + (int64_t)(b ? rowB : rowA) * N2 + jj;
+                const uint32_t off = (uint32_t)((b ? rowB : rowA) * N2 + jj) * 8u;
 #pragma unroll
-                for (int q = 0; q < RF0; ++q) dst[q * LR] = v[ib * RF0 + q];
+                for (int q = 0; q < RF0; ++q) Y.st2(v[ib * RF0 + q], off, q * LR * 8);
             }
         }
         if (mask) {
-            cf *V = k.Ym + (int64_t)pr * k.N;
+            const Buf V(k.Ym + (int64_t)pr * k.N, pbytes);
+            const Buf Ms(k.Mspec, pbytes);
 #pragma unroll
-            for (int i = 0; i < E; ++i) {
-                int b, k2;
-                FF::template where<RFL>(i, tid, b, k2);
+            for (int ib = 0; ib < E / RFL; ++ib) {
+                const int jg = tid + ib * T, b = jg / LRL, jj = jg - b * LRL;
                 const int row = b ? rowB : rowA;
-                const cf M = k.Mspec[(int64_t)row * N2 + k2];
-                v[i] = mask_ramp(k, ra, rb, row + (int64_t)N1 * k2, M);
+                const int64_t kb0 = row + (int64_t)N1 * jj;
+                const uint64_t p0a = (uint64_t)kb0 * rwa, p0b = (uint64_t)kb0 * rwb;
+                const uint32_t moff = (uint32_t)(row * N2 + jj) * 8u;
+#pragma unroll
+                for (int q = 0; q < RFL; ++q) {
+                    const int i = ib * RFL + q;
+                    const cf M = Ms.ld2(moff, q * LRL * 8);
+                    if constexpr (kAbl & 8) {
+                        v[i] = M;
+                    } else if (kb0 == 0 && 2 * q == RFL) {          // Nyquist bin
+                        v[i] = make_float2(M.x * k.p.nyq_im[ra], M.x * k.p.nyq_im[rb]);
+                    } else if (kb0 == 0 && q == 0) {                // DC: M (1 + i)
+                        v[i] = make_float2(M.x - M.y, M.y + M.x);
+                    } else {                                        // M (R_a + i R_b)
+                        const cf Ra = ramp_q<RFL>(p0a, sta, nwa, q), Rb = ramp_q<RFL>(p0b, stb, nwb, q);
+                        v[i] = cmul(M, make_float2(Ra.x - Rb.y, Ra.y + Rb.x));
+                    }
+                }
             }
             __syncthreads();
-            FF::template run<true, 1, I...>(v, lds, tid);
+            if constexpr (!(kAbl & 2)) FF::template run<true, 1, I...>(v, lds, tid);
 #pragma unroll
             for (int ib = 0; ib < E / RF0; ++ib) {
                 const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
-                cf *dst = V + (int64_t)(b ? rowB : rowA) * N2 + jj;
+                const uint32_t off = (uint32_t)((b ? rowB : rowA) * N2 + jj) * 8u;
 #pragma unroll
-                for (int q = 0; q < RF0; ++q) dst[q * LR] = v[ib * RF0 + q];
+                for (int q = 0; q < RF0; ++q) V.st2(v[ib * RF0 + q], off, q * LR * 8);
             }
         }
     }
@@ -706,8 +745,10 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
             const int b4 = (it - n1 * (B / 4)) * 4;
             const int64_t n = n1 * N2 + n20 + b4;
             float xa[4], xb[4], dum[4];
+            if (kAbl & 1) { for (int q = 0; q < 4; ++q) xa[q] = (float)(n + q); } else
             if (hasa) source4(k, ra, n, 4, xa, dum, true, false);
             else { xa[0] = xa[1] = xa[2] = xa[3] = 0.f; }
+            if (kAbl & 1) { for (int q = 0; q < 4; ++q) xb[q] = (float)(n - q); } else
             if (hasb) source4(k, rb, n, 4, xb, dum, true, false);
             else { xb[0] = xb[1] = xb[2] = xb[3] = 0.f; }
 #pragma unroll
@@ -717,7 +758,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         cf v[E];
         FF::template load<RF0>(v, lds, tid);
         __syncthreads();
-        FF::template run<false, 1, F...>(v, lds, tid);
+        if constexpr (!(kAbl & 2)) FF::template run<false, 1, F...>(v, lds, tid);
         const float invN = k.invN;
 #pragma unroll
         for (int i = 0; i < E; ++i) {
@@ -726,7 +767,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
             const int64_t m = (n20 + b) * (int64_t)k1;
             float rev = (float)m * invN;
             if (rev >= 0.5f) rev -= 1.0f;
-            v[i] = cmul(v[i], expi_rev(-rev));
+            if constexpr (!(kAbl & 4)) v[i] = cmul(v[i], expi_rev(-rev)); else v[i] = v[i];
         }
         FF::template store<RFL>(v, lds, tid);
         __syncthreads();
@@ -742,9 +783,9 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         }
     }
 
-    // inverse column FFTs of one spilled pair block into (re, im) per item
-    __device__ static void inv_block(const KP &k, const cf *Yp, int64_t n20, cf *lds, int tid,
-                                     float (&re)[ITEMS][4], float (&im)[ITEMS][4]) {
+    // inverse column FFTs of one spilled pair block; result left in LDS in
+    // natural order (Lds<N1>::at(column, n1)), unscaled
+    __device__ static void inv_block(const KP &k, const cf *Yp, int64_t n20, cf *lds, int tid) {
         const int64_t N2 = k.N2;
         const float invN = k.invN;
         for (int it = tid; it < N1 * B / 4; it += T) {
@@ -759,32 +800,21 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
                 const int64_t m = (n20 + b4 + i) * (int64_t)k1;
                 float rev = (float)m * invN;
                 if (rev >= 0.5f) rev -= 1.0f;
-                lds[Lds<N1>::at(b4 + i, k1)] = cmul(a[i], expi_rev(rev));
+                if constexpr (!(kAbl & 4)) lds[Lds<N1>::at(b4 + i, k1)] = cmul(a[i], expi_rev(rev)); else lds[Lds<N1>::at(b4 + i, k1)] = a[i];
             }
         }
         __syncthreads();
         cf v[E];
         FF::template load<RI0>(v, lds, tid);
         __syncthreads();
-        FF::template run<true, 1, I...>(v, lds, tid);
+        if constexpr (!(kAbl & 2)) FF::template run<true, 1, I...>(v, lds, tid);
         FF::template store<RIL>(v, lds, tid);
-        __syncthreads();
-#pragma unroll
-        for (int t = 0; t < ITEMS; ++t) {
-            const int it = tid + t * T;
-            const int n1 = it / (B / 4);
-            const int b4 = (it - n1 * (B / 4)) * 4;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const cf z = lds[Lds<N1>::at(b4 + i, n1)];
-                re[t][i] = z.x * invN;
-                im[t][i] = z.y * invN;
-            }
-        }
         __syncthreads();
     }
 
-    // C: inverse column FFTs of the data pair (and mask pair), epilogues of a, b
+    // C: inverse column FFTs of the mask pair (kept as one threshold bit per
+    // value: only mask > 1 is used downstream) and of the data pair, then the
+    // epilogues of channels a, b straight from LDS.
     __device__ static void passC(const KP &k) {
         __shared__ cf lds[B * Lds<N1>::RS];
         const int tid = threadIdx.x;
@@ -794,21 +824,48 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         const int64_t n20 = (int64_t)blockIdx.x * B;
         const bool data = k.p.data_in_fft != 0;
         const bool mask = k.p.null_mode == PSS_NULL_DELAYED;
-        float da[ITEMS][4], db[ITEMS][4], ma[ITEMS][4], mb[ITEMS][4];
+        const float invN = k.invN;
+        static_assert(ITEMS * 8 <= 32, "mask bits per thread");
+        uint32_t bits = 0;
+        if (mask) {
+            inv_block(k, k.Ym + (int64_t)pr * k.N, n20, lds, tid);
 #pragma unroll
-        for (int t = 0; t < ITEMS; ++t)
+            for (int t = 0; t < ITEMS; ++t) {
+                const int it = tid + t * T;
+                const int n1 = it / (B / 4);
+                const int b4 = (it - n1 * (B / 4)) * 4;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { da[t][i] = db[t][i] = ma[t][i] = mb[t][i] = 0.f; }
-        if (data) inv_block(k, k.Yd + (int64_t)pr * k.N, n20, lds, tid, da, db);
-        if (mask) inv_block(k, k.Ym + (int64_t)pr * k.N, n20, lds, tid, ma, mb);
-#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const cf z = lds[Lds<N1>::at(b4 + i, n1)];
+                    bits |= (uint32_t)(z.x * invN > 1.0f) << (8 * t + i);
+                    bits |= (uint32_t)(z.y * invN > 1.0f) << (8 * t + 4 + i);
+                }
+            }
+            __syncthreads();
+        }
+        if (data) inv_block(k, k.Yd + (int64_t)pr * k.N, n20, lds, tid);
+#pragma unroll 1
         for (int t = 0; t < ITEMS; ++t) {
             const int it = tid + t * T;
             const int n1 = it / (B / 4);
             const int b4 = (it - n1 * (B / 4)) * 4;
             const int64_t n = n1 * k.N2 + n20 + b4;
-            if (hasa) epilogue4(k, ra, n, 4, da[t], ma[t], !data);
-            if (hasb) epilogue4(k, rb, n, 4, db[t], mb[t], !data);
+            float da[4], db[4], ma[4], mb[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (data) {
+                    const cf z = lds[Lds<N1>::at(b4 + i, n1)];
+                    da[i] = z.x * invN;
+                    db[i] = z.y * invN;
+                } else {
+                    da[i] = db[i] = 0.f;
+                }
+                ma[i] = ((bits >> (8 * t + i)) & 1u) ? 2.0f : 0.0f;
+                mb[i] = ((bits >> (8 * t + 4 + i)) & 1u) ? 2.0f : 0.0f;
+            }
+            if (kAbl & 1) { *reinterpret_cast<float4 *>(k.p.data + (int64_t)ra * k.p.ld + n) = make_float4(da[0] + ma[0], da[1], da[2], da[3]); *reinterpret_cast<float4 *>(k.p.data + (int64_t)rb * k.p.ld + n) = make_float4(db[0] + mb[0], db[1], db[2], db[3]); continue; }
+            if (hasa) epilogue4(k, ra, n, 4, da, ma, !data);
+            if (hasb) epilogue4(k, rb, n, 4, db, mb, !data);
         }
     }
 };
@@ -995,6 +1052,8 @@ static int launch_single(const KP &k, hipStream_t st) {
 }
 
 // Column plans: B*N1 = 8192 complex per workgroup, 512 threads, 16 per thread.
+// Inverse plans (..I) mirror the forward ones where registers carry over
+// (single pass, rows); column inverses start from LDS and reuse the forward plan.
 // Row plans: N2 = 8192 (1 row, 512 thr) or N2 <= 4096 (4096/N2 rows, 256 thr).
 using C16 = RList<16>;
 using C32F = RList<16, 2>;
@@ -1011,8 +1070,8 @@ using C1kI = RList<4, 16, 16>;
 using C2kF = RList<16, 16, 8>;
 using C2kI = RList<8, 16, 16>;
 using C4k = RList<16, 16, 16>;
-using C8kF = RList<16, 16, 16, 2>;
-using C8kI = RList<2, 16, 16, 16>;
+using C8kF = RList<16, 8, 8, 8>;
+using C8kI = RList<8, 8, 8, 16>;
 
 template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typename RF, typename RI,
           int TRF>
@@ -1070,7 +1129,7 @@ static int run_fourstep(KP &k, hipStream_t st, float *mask_row) {
         switch (k.N1) {
 #define CASE8K(N1_, CF, CI)                                                                          \
     case N1_:                                                                                        \
-        return launch_pair<N1_, 8192 / N1_, 512, CF, CI, 8192, 1024, C8kF, C8kI, 512>(k, st, mask_row);
+        return launch_pair<N1_, 8192 / N1_, 512, CF, CF, 8192, 1024, C8kF, C8kI, 512>(k, st, mask_row);
             CASE8K(16, C16, C16)
             CASE8K(32, C32F, C32I)
             CASE8K(64, C64F, C64I)
@@ -1142,6 +1201,7 @@ static int validate(const PssPipeline *p) {
     if (p->nchan > 65535) return fail(PSS_EINVAL, "nchan %d > 65535 per launch", p->nchan);
     if (!p->data) return fail(PSS_EINVAL, "data is NULL");
     if (p->ld < p->nsamp) return fail(PSS_EINVAL, "ld < nsamp");
+    if (p->nsamp >= (1ll << 31)) return fail(PSS_EUNSUPPORTED, "nsamp >= 2^31");
     if (p->src == PSS_SRC_SEARCH && (!p->prof || p->nint < 1 || p->knot_m < 1))
         return fail(PSS_EINVAL, "search source needs a PCHIP table");
     if (p->src == PSS_SRC_FOLD && (!p->prof || p->nph < 1))
