@@ -41,9 +41,12 @@ LOG2N = 22
 TOBS_PER_SAMPLE = 20.48e-6
 
 # algorithmic HBM bytes per channel-sample of each kernel in the C3 run
-# (complex64 spill = 8 B, real fp32 in/out = 4 B; DESIGN.md "Roofline")
-ALG_BYTES = {"fourstep_colA": 8.0, "fourstep_row": 16.0, "fourstep_colC": 12.0,
-             "single_pass": 4.0, "elementwise": 4.0, "fallback_dft": 28.0}
+# (DESIGN.md "Roofline"): the four-step spill holds two channels per complex64
+# value (pair mode), i.e. 4 B per channel-sample per spill pass; the null mask
+# is a once-per-run table (no per-channel bytes).
+#   colA: write spill 4 | row: read 4 + write 4 | colC: read spill 4 + write fp32 4
+ALG_BYTES = {"fourstep_colA": 4.0, "fourstep_row": 8.0, "fourstep_colC": 8.0,
+             "single_pass": 4.0, "elementwise": 8.0, "fallback_dft": 28.0}
 
 
 def c3_step(pss, nchan_total, shard, nsamp_log2, ret_out=False):

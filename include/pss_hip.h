@@ -133,6 +133,13 @@ typedef struct PssPipeline {
     const float *inj_box;     /* [nsamp] box values (already scaled), shared    */
     const float *inj_rep;     /* [nchan][nsamp] DELAYED replacement values      */
     const float *inj_noise;   /* [nchan][nsamp] noise chi2 draws                */
+
+    /* DELAYED null: [nchan] frac(s_mask/N) in 2^-64 cycles, s_mask = the
+       signal's total delay in samples (pulsar.py:322-325).  Four-step lengths
+       (N = 2^m >= 2^14) decide mask > 1 from a once-per-run table of the box
+       row shifted by the fraction of s_mask; the other
+       lengths use `ramp`/`nyq_im` and carry the mask through the FFT.       */
+    const uint64_t *mask_ramp;
 } PssPipeline;
 
 /* Library / device info. */

@@ -203,6 +203,7 @@ def plan_pipeline(sig, pend, rows, chan0):
         if nul is not None and nul["mode"] == "delayed":
             mask_total = nul["mask_samples"]
             nyq_im = np.cos(np.pi * mask_total)
+            A["mask_ramp"] = ramp_words(mask_total[gidx], N)
             if pend.shifts:
                 P["data_in_fft"], ramp_s = 1, total
             else:
@@ -250,7 +251,7 @@ def build_pipeline(sig, pend, rows, chan0, data, out=None):
             src.dev_table = to_dev(src.table)
         p.prof = ptr(src.dev_table)
     for name, arr in P["arrays"].items():
-        t = u64_to_i64_tensor(arr) if name == "ramp" else to_dev(arr)
+        t = u64_to_i64_tensor(arr) if name in ("ramp", "mask_ramp") else to_dev(arr)
         keep.append(t)
         setattr(p, name, ptr(t))
     if P.get("shift"):

@@ -39,6 +39,7 @@ class PssPipeline(ctypes.Structure):
         ("out_kind", c_i32), ("out", c_vp), ("clip", c_f32),
         ("seed", c_u64), ("call_gen", c_u32), ("call_null", c_u32), ("call_noise", c_u32),
         ("inj_gen", c_vp), ("inj_box", c_vp), ("inj_rep", c_vp), ("inj_noise", c_vp),
+        ("mask_ramp", c_vp),
     ]
 
 

@@ -96,9 +96,87 @@ struct KP {
     int npairs;
     int poff;       // chan0 & 1: pairs are (even, odd) GLOBAL channels
     cf *Yd;         // data pair spill    [npairs][N1][N2]
-    cf *Ym;         // mask pair spill    [npairs][N1][N2]
+    cf *Ym;         // node pair spill    [KCH/2][N1][N2] (mask table build)
     const cf *Mspec;// mask spectrum      [N1][N2] (natural k2 per row k1)
+    // delayed-null mask table (four-step lengths; see k_mask_table)
+    int mtab;               // 1: mask decisions come from the table
+    int log2n;
+    const uint4 *mt_bits;   // [N/64] {ambiguous bits lo/hi, nulled bits lo/hi}
+    const uint32_t *mt_base;// [N/64] index of the block's first ambiguous position
+    const float *mt_coef;   // [n_ambiguous][KCH] Chebyshev coefficients in t
 };
+
+// ---------------------------------------------------------------------------
+// Delayed-null mask table.
+//
+// The reference shifts ONE box row (the same for every channel) by each
+// channel's total delay s_c and nulls where the result exceeds 1
+// (pulsar.py:306-330).  Write s = i + f (i integer, f in [0,1)).  For integer
+// sample offsets d the shift_t kernel, Nyquist rule included, satisfies
+// h_s(d) = h_f(d - i): the integer part is an exact circular roll, so
+//     mask_c[n] = M(p, f_c),  p = (n - i_c) mod N,
+// with M(p, f) = shift_t(box, f)[p] one function of (p, f) for all channels.
+// As a function of f, M(p, .) is a trigonometric polynomial of bandwidth
+// pi (bins |k| <= N/2), so a degree-11 Chebyshev interpolant in t = 2f - 1
+// from KCH = 12 node shifts is exact to ~1e-9 relative (tools: DESIGN.md §3).
+// Per position the table stores whether M > 1 for EVERY f (bound
+// c0 -+ sum|c_n|), for NO f, or -- for the ~2% of positions near box edges
+// where the answer depends on f -- the 12 coefficients.  The node shifts are
+// KCH/2 pair rows through the same FFT engine, once per run; per channel
+// nothing but a table lookup remains (no per-channel mask FFT or spill).
+// ---------------------------------------------------------------------------
+static constexpr int KCH = 12;
+
+// t = 2 f - 1 and i from the mask ramp word w = frac(s / N) 2^64 (N = 2^L)
+__device__ __forceinline__ void mask_split(uint64_t w, int L, uint32_t &ishift, float &t) {
+    ishift = (uint32_t)(w >> (64 - L));
+    const uint64_t fr = w << L;                         // f in 2^-64 units
+    t = fmaf((float)(uint32_t)(fr >> 40), 1.1920928955078125e-07f, -1.0f);   // 2 f - 1
+}
+
+__device__ __forceinline__ float cheb_eval(const float *c, float t) {
+    const float4 a = reinterpret_cast<const float4 *>(c)[0];
+    const float4 b = reinterpret_cast<const float4 *>(c)[1];
+    const float4 d = reinterpret_cast<const float4 *>(c)[2];
+    const float cc[KCH] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, d.x, d.y, d.z, d.w};
+    const float t2 = 2.0f * t;
+    float b1 = 0.f, b2 = 0.f;
+#pragma unroll
+    for (int n = KCH - 1; n >= 1; --n) {
+        const float b0 = fmaf(t2, b1, cc[n] - b2);
+        b2 = b1;
+        b1 = b0;
+    }
+    return fmaf(t, b1, cc[0] - b2);
+}
+
+// Null decision bits (bit i: sample n0 + i) for 4 consecutive samples of a
+// channel with mask split (ishift, t).
+__device__ __forceinline__ uint32_t mask_hits4(const KP &k, int64_t n0, uint32_t ishift, float t) {
+    const uint32_t nm = (uint32_t)k.N - 1u;
+    const uint32_t p0 = ((uint32_t)n0 - ishift) & nm;
+    const uint32_t w0 = p0 >> 6, w3 = ((p0 + 3u) & nm) >> 6;
+    const uint4 W0 = k.mt_bits[w0];
+    const uint4 W3 = (w3 == w0) ? W0 : k.mt_bits[w3];
+    if (((W0.x | W0.y | W0.z | W0.w) | (W3.x | W3.y | W3.z | W3.w)) == 0u) return 0u;
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t p = (p0 + (uint32_t)i) & nm;
+        const bool first = (p >> 6) == w0;
+        const uint4 W = first ? W0 : W3;
+        const uint32_t b = p & 63u;
+        const uint64_t amb = ((uint64_t)W.y << 32) | W.x;
+        const uint64_t hi = ((uint64_t)W.w << 32) | W.z;
+        bool hit = (hi >> b) & 1u;
+        if ((amb >> b) & 1u) {
+            const uint32_t idx = k.mt_base[p >> 6] + (uint32_t)__popcll(amb & ((1ull << b) - 1ull));
+            hit = cheb_eval(k.mt_coef + (int64_t)idx * KCH, t) > 1.0f;
+        }
+        r |= (uint32_t)hit << i;
+    }
+    return r;
+}
 
 __device__ __forceinline__ int64_t floordiv(int64_t a, int64_t b) {
     int64_t q = a / b;
@@ -318,15 +396,25 @@ __device__ __forceinline__ cf apply_ramp(const KP &k, int r, int64_t kb, cf z) {
 // ---------------------------------------------------------------------------
 // path 0: no FFT -- source -> null(undelayed) -> epilogue, one pass
 // ---------------------------------------------------------------------------
+// With k.mtab (delayed null on a four-step length whose data needs no delay
+// in this run) the mask decisions come from the mask table.
 __global__ __launch_bounds__(256) void k_elementwise(KP k) {
     const int r = blockIdx.y;
     const int64_t items = (k.N + 3) >> 2;
+    uint32_t is = 0;
+    float t = 0.f;
+    if (k.mtab) mask_split((uint64_t)k.p.mask_ramp[r], k.log2n, is, t);
     for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < items;
          it += (int64_t)gridDim.x * blockDim.x) {
         const int64_t n0 = it << 2;
         const int cnt = (int)min((int64_t)4, k.N - n0);
         float re[4], im[4];
-        source4(k, r, n0, cnt, re, im, true);
+        source4(k, r, n0, cnt, re, im, true, !k.mtab);
+        if (k.mtab) {
+            const uint32_t h = mask_hits4(k, n0, is, t);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) im[i] = ((h >> i) & 1u) ? 2.0f : 0.0f;
+        }
         epilogue4(k, r, n0, cnt, re, im, false);
     }
 }
@@ -609,6 +697,10 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
     static constexpr int LR = N2 / RF0;
     static constexpr int LRL = N2 / RFL;
 
+    // MASK = false: data pair of channels (2pr - poff, 2pr + 1 - poff).
+    // MASK = true : node pair (2pr, 2pr + 1) of the mask table build -- the
+    //               once-per-run mask spectrum times each node's ramp.
+    template <bool MASK>
     __device__ static void pass(const KP &k) {
         __shared__ cf lds[2 * Lds<N2>::RS];
         const int tid = threadIdx.x;
@@ -616,9 +708,10 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
         const int j = blockIdx.y;                  // row pair {j, N1-j}; {0, N1/2}
         const int N1 = (int)k.N1;
         const int rowA = j, rowB = (j == 0) ? N1 / 2 : N1 - j;
-        const int ra = max(2 * pr - k.poff, 0), rb = min(2 * pr + 1 - k.poff, k.p.nchan - 1);
-        const bool data = k.p.data_in_fft != 0;
-        const bool mask = k.p.null_mode == PSS_NULL_DELAYED;
+        const int off = MASK ? 0 : k.poff;
+        const int ra = max(2 * pr - off, 0), rb = min(2 * pr + 1 - off, k.p.nchan - 1);
+        const bool data = !MASK;
+        const bool mask = MASK;
         const uint64_t rwa = (uint64_t)k.p.ramp[ra], rwb = (uint64_t)k.p.ramp[rb];
         // uniform 64-bit phase offsets of bin kb0 + q N/RFL relative to kb0 (SALU)
         const uint64_t sta = (uint64_t)(k.N / RFL) * rwa, stb = (uint64_t)(k.N / RFL) * rwb;
@@ -715,7 +808,9 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
 };
 
 template <typename R, int T>
-__global__ __launch_bounds__(T) void k_pair_row(KP k) { R::pass(k); }
+__global__ __launch_bounds__(T) void k_pair_row(KP k) { R::template pass<false>(k); }
+template <typename R, int T>
+__global__ __launch_bounds__(T) void k_node_row(KP k) { R::template pass<true>(k); }
 
 template <int N1, int B, int T, typename FWD, typename INV>
 struct PairCols;
@@ -812,9 +907,8 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         __syncthreads();
     }
 
-    // C: inverse column FFTs of the mask pair (kept as one threshold bit per
-    // value: only mask > 1 is used downstream) and of the data pair, then the
-    // epilogues of channels a, b straight from LDS.
+    // C: inverse column FFTs of the data pair, then the epilogues of channels
+    // a, b straight from LDS (delayed-null decisions from the mask table).
     __device__ static void passC(const KP &k) {
         __shared__ cf lds[B * Lds<N1>::RS];
         const int tid = threadIdx.x;
@@ -822,28 +916,15 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         const int ra = 2 * pr - k.poff, rb = ra + 1;
         const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
         const int64_t n20 = (int64_t)blockIdx.x * B;
-        const bool data = k.p.data_in_fft != 0;
-        const bool mask = k.p.null_mode == PSS_NULL_DELAYED;
+        const bool mask = k.mtab != 0;
         const float invN = k.invN;
-        static_assert(ITEMS * 8 <= 32, "mask bits per thread");
-        uint32_t bits = 0;
+        uint32_t isa = 0, isb = 0;
+        float ta = 0.f, tb = 0.f;
         if (mask) {
-            inv_block(k, k.Ym + (int64_t)pr * k.N, n20, lds, tid);
-#pragma unroll
-            for (int t = 0; t < ITEMS; ++t) {
-                const int it = tid + t * T;
-                const int n1 = it / (B / 4);
-                const int b4 = (it - n1 * (B / 4)) * 4;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const cf z = lds[Lds<N1>::at(b4 + i, n1)];
-                    bits |= (uint32_t)(z.x * invN > 1.0f) << (8 * t + i);
-                    bits |= (uint32_t)(z.y * invN > 1.0f) << (8 * t + 4 + i);
-                }
-            }
-            __syncthreads();
+            if (hasa) mask_split((uint64_t)k.p.mask_ramp[ra], k.log2n, isa, ta);
+            if (hasb) mask_split((uint64_t)k.p.mask_ramp[rb], k.log2n, isb, tb);
         }
-        if (data) inv_block(k, k.Yd + (int64_t)pr * k.N, n20, lds, tid);
+        inv_block(k, k.Yd + (int64_t)pr * k.N, n20, lds, tid);
 #pragma unroll 1
         for (int t = 0; t < ITEMS; ++t) {
             const int it = tid + t * T;
@@ -851,21 +932,45 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
             const int b4 = (it - n1 * (B / 4)) * 4;
             const int64_t n = n1 * k.N2 + n20 + b4;
             float da[4], db[4], ma[4], mb[4];
+            const uint32_t ha = (mask && hasa) ? mask_hits4(k, n, isa, ta) : 0u;
+            const uint32_t hb = (mask && hasb) ? mask_hits4(k, n, isb, tb) : 0u;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                if (data) {
-                    const cf z = lds[Lds<N1>::at(b4 + i, n1)];
-                    da[i] = z.x * invN;
-                    db[i] = z.y * invN;
-                } else {
-                    da[i] = db[i] = 0.f;
-                }
-                ma[i] = ((bits >> (8 * t + i)) & 1u) ? 2.0f : 0.0f;
-                mb[i] = ((bits >> (8 * t + 4 + i)) & 1u) ? 2.0f : 0.0f;
+                const cf z = lds[Lds<N1>::at(b4 + i, n1)];
+                da[i] = z.x * invN;
+                db[i] = z.y * invN;
+                ma[i] = ((ha >> i) & 1u) ? 2.0f : 0.0f;
+                mb[i] = ((hb >> i) & 1u) ? 2.0f : 0.0f;
             }
             if (kAbl & 1) { *reinterpret_cast<float4 *>(k.p.data + (int64_t)ra * k.p.ld + n) = make_float4(da[0] + ma[0], da[1], da[2], da[3]); *reinterpret_cast<float4 *>(k.p.data + (int64_t)rb * k.p.ld + n) = make_float4(db[0] + mb[0], db[1], db[2], db[3]); continue; }
-            if (hasa) epilogue4(k, ra, n, 4, da, ma, !data);
-            if (hasb) epilogue4(k, rb, n, 4, db, mb, !data);
+            if (hasa) epilogue4(k, ra, n, 4, da, ma, false);
+            if (hasb) epilogue4(k, rb, n, 4, db, mb, false);
+        }
+    }
+
+    // Mask table build: inverse column FFTs of node pair `blockIdx.y`, stored
+    // (scaled) as node rows nodes[2 pr], nodes[2 pr + 1].
+    __device__ static void node_col(const KP &k, float *nodes) {
+        __shared__ cf lds[B * Lds<N1>::RS];
+        const int tid = threadIdx.x;
+        const int pr = blockIdx.y;
+        const int64_t n20 = (int64_t)blockIdx.x * B;
+        const float invN = k.invN;
+        inv_block(k, k.Ym + (int64_t)pr * k.N, n20, lds, tid);
+        float *ra = nodes + (int64_t)(2 * pr) * k.N, *rb = ra + k.N;
+        for (int it = tid; it < N1 * B / 4; it += T) {
+            const int n1 = it / (B / 4);
+            const int b4 = (it - n1 * (B / 4)) * 4;
+            const int64_t n = n1 * k.N2 + n20 + b4;
+            float a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const cf z = lds[Lds<N1>::at(b4 + i, n1)];
+                a[i] = z.x * invN;
+                b[i] = z.y * invN;
+            }
+            *reinterpret_cast<float4 *>(ra + n) = make_float4(a[0], a[1], a[2], a[3]);
+            *reinterpret_cast<float4 *>(rb + n) = make_float4(b[0], b[1], b[2], b[3]);
         }
     }
 };
@@ -874,6 +979,68 @@ template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairA(KP k) { C::passA(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairC(KP k) { C::passC(k); }
+template <typename C, int T>
+__global__ __launch_bounds__(T) void k_node_col(KP k, float *nodes) { C::node_col(k, nodes); }
+
+// Node ramps of the mask table: f_j = (t_j + 1)/2 at the Chebyshev points
+// t_j = cos(pi (j + 1/2) / KCH); ramp word f_j / N * 2^64, Nyquist cos(pi f_j).
+__global__ void k_node_params(uint64_t *ramp, float *nyq, int L) {
+    const int j = threadIdx.x;
+    if (j < KCH) {
+        const double t = cospi((j + 0.5) / KCH);
+        const double f = 0.5 * (t + 1.0);
+        ramp[j] = (uint64_t)ldexp(f, 64 - L);
+        nyq[j] = (float)cospi(f);
+    }
+}
+
+// Per position p: Chebyshev coefficients of M(p, t) from the KCH node values,
+// classification (never / always / depends-on-f nulled) with the bound
+// |M - c0| <= sum_{n>=1} |c_n| on t in [-1, 1], and compaction of the
+// coefficients of the f-dependent positions (wave ballot + one atomic per
+// wave; positions are self-describing, so the atomic order does not matter).
+__global__ __launch_bounds__(256) void k_mask_table(const float *nodes, int64_t N, uint4 *bits,
+                                                    uint32_t *base, float *coef, uint32_t *counter) {
+    __shared__ float T[KCH * KCH];
+    if (threadIdx.x < KCH * KCH) {
+        const int n = threadIdx.x / KCH, j = threadIdx.x - n * KCH;
+        T[threadIdx.x] = (float)(cospi((double)n * (j + 0.5) / KCH) * (n ? 2.0 : 1.0) / KCH);
+    }
+    __syncthreads();
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // N % 256 == 0
+    float v[KCH], c[KCH];
+#pragma unroll
+    for (int j = 0; j < KCH; ++j) v[j] = nodes[(int64_t)j * N + p];
+    float S = 0.f;
+#pragma unroll
+    for (int n = 0; n < KCH; ++n) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < KCH; ++j) s = fmaf(T[n * KCH + j], v[j], s);
+        c[n] = s;
+        if (n) S += fabsf(s);
+    }
+    // margin covers the fp32 evaluation error of cheb_eval (~1e-6 sum|c|)
+    const float eps = 1e-3f + 4e-6f * (fabsf(c[0]) + S);
+    const bool hi = c[0] - S > 1.0f + eps;
+    const bool amb = !hi && !(c[0] + S < 1.0f - eps);
+    const uint64_t ab = __ballot(amb), hb = __ballot(hi);
+    const int lane = threadIdx.x & 63;
+    uint32_t b0 = 0;
+    if (lane == 0 && ab) b0 = atomicAdd(counter, (uint32_t)__popcll(ab));
+    b0 = __shfl(b0, 0);
+    if (lane == 0) {
+        bits[p >> 6] = make_uint4((uint32_t)ab, (uint32_t)(ab >> 32), (uint32_t)hb, (uint32_t)(hb >> 32));
+        base[p >> 6] = b0;
+    }
+    if (amb) {
+        const uint32_t idx = b0 + (uint32_t)__popcll(ab & ((1ull << lane) - 1ull));
+        float4 *dst = reinterpret_cast<float4 *>(coef + (int64_t)idx * KCH);
+        dst[0] = make_float4(c[0], c[1], c[2], c[3]);
+        dst[1] = make_float4(c[4], c[5], c[6], c[7]);
+        dst[2] = make_float4(c[8], c[9], c[10], c[11]);
+    }
+}
 
 // ---------------------------------------------------------------------------
 // path 3: direct DFT fallback for even N that are not handled above.
@@ -1073,43 +1240,135 @@ using C4k = RList<16, 16, 16>;
 using C8kF = RList<16, 8, 8, 8>;
 using C8kI = RList<8, 8, 8, 16>;
 
+// ---------------------------------------------------------------------------
+// workspace layout (every region 256-B aligned)
+//   four-step (N = 2^m, 2^14 <= N <= 2^24):
+//     Yd [npairs][N] cf | Mspec [N] cf | node spill [KCH/2][N] cf |
+//     nodes [KCH][N] f32 | table bits [N/64] uint4 | base [N/64] u32 |
+//     coef [N][KCH] f32 (worst case) | misc (counter, node ramps/nyq) | mask row [N] f32
+//   single pass (N <= 8192): mask row
+//   direct DFT fallback: W1, W2 [nchan][N] cf | twiddles [N] cf | mask row
+// ---------------------------------------------------------------------------
+static inline int64_t al256(int64_t b) { return (b + 255) & ~255ll; }
+static inline bool fourstep_len(int64_t n) { return is_pow2(n) && n >= 16384 && n <= (1ll << 24); }
+
+struct WsLayout {
+    int64_t yd, mspec, ynode, nodes, bits, base, coef, misc, row, total;
+};
+
+static WsLayout ws_layout(int32_t nchan, int64_t N) {
+    WsLayout w;
+    memset(&w, 0, sizeof(w));
+    int64_t o = 0;
+    if (fourstep_len(N)) {
+        const int64_t npairs = ((int64_t)nchan + 2) / 2;   // pairs of (even, odd) global channels
+        w.yd = o;    o += al256(npairs * N * 8);
+        w.mspec = o; o += al256(N * 8);
+        w.ynode = o; o += al256((int64_t)(KCH / 2) * N * 8);
+        w.nodes = o; o += al256((int64_t)KCH * N * 4);
+        w.bits = o;  o += al256((N / 64) * 16);
+        w.base = o;  o += al256((N / 64) * 4);
+        w.coef = o;  o += al256(N * KCH * 4);
+        w.misc = o;  o += 256;
+    } else if (!(is_pow2(N) && N >= 64 && N <= 8192)) {
+        o += al256(2 * (int64_t)nchan * N * 8 + N * 8);    // fallback: W1, W2, twiddles
+    }
+    w.row = o;
+    o += al256(N * 4);
+    w.total = o;
+    return w;
+}
+
+// Mask table of a delayed null (see the comment above KCH): mask spectrum,
+// KCH node shifts (KCH/2 pair rows through the row and column engines),
+// Chebyshev coefficients + classification.  Once per run, channel independent.
 template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typename RF, typename RI,
           int TRF>
-static int launch_pair(KP &k, hipStream_t st, float *mask_row) {
+static int build_mask_table(KP &k, hipStream_t st, const float *mask_row, char *w, const WsLayout &L) {
+    using PC = PairCols<N1, B, T, CF, CI>;
+    using PR = PairRows<N2, TR, RF, RI>;
+    cf *mspec = reinterpret_cast<cf *>(w + L.mspec);
+    uint32_t *counter = reinterpret_cast<uint32_t *>(w + L.misc);
+    uint64_t *nramp = reinterpret_cast<uint64_t *>(w + L.misc + 64);
+    float *nnyq = reinterpret_cast<float *>(w + L.misc + 192);
+    float *nodes = reinterpret_cast<float *>(w + L.nodes);
+    int log2n = 0;
+    while ((1ll << log2n) < k.N) ++log2n;
+    // spectrum of the (channel independent) mask row
+    KP km = k;
+    km.p.nchan = 1;
+    km.p.chan0 = 0;
+    km.p.data = const_cast<float *>(mask_row);
+    km.p.ld = k.N;
+    km.p.src = PSS_SRC_LOAD;
+    km.p.null_mode = PSS_NULL_NONE;
+    km.p.data_in_fft = 1;
+    km.p.work = mspec;
+    using C1 = Cols<N1, B, T, CF, CI>;
+    using R1 = Rows<N2, 1, TRF, RF, RI, true>;
+    k_colA<C1, T><<<dim3((unsigned)(N2 / B), 1), dim3(T), 0, st>>>(km);
+    LAUNCHCHK();
+    k_row<R1, TRF><<<dim3((unsigned)N1, 1), dim3(TRF), 0, st>>>(km);
+    LAUNCHCHK();
+    // node shifts
+    k_node_params<<<1, 64, 0, st>>>(nramp, nnyq, log2n);
+    LAUNCHCHK();
+    KP kn = k;
+    kn.p.nchan = KCH;
+    kn.p.chan0 = 0;
+    kn.p.ramp = nramp;
+    kn.p.nyq_re = nnyq;
+    kn.p.nyq_im = nnyq;
+    kn.poff = 0;
+    kn.npairs = KCH / 2;
+    kn.Ym = reinterpret_cast<cf *>(w + L.ynode);
+    kn.Mspec = mspec;
+    k_node_row<PR, TR><<<dim3((unsigned)(KCH / 2), (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(kn);
+    LAUNCHCHK();
+    k_node_col<PC, T><<<dim3((unsigned)(N2 / B), (unsigned)(KCH / 2)), dim3(T), 0, st>>>(kn, nodes);
+    LAUNCHCHK();
+    // table
+    HIPCHK(hipMemsetAsync(counter, 0, 4, st));
+    k.mt_bits = reinterpret_cast<const uint4 *>(w + L.bits);
+    k.mt_base = reinterpret_cast<const uint32_t *>(w + L.base);
+    k.mt_coef = reinterpret_cast<const float *>(w + L.coef);
+    k_mask_table<<<dim3((unsigned)(k.N / 256)), dim3(256), 0, st>>>(
+        nodes, k.N, reinterpret_cast<uint4 *>(w + L.bits), reinterpret_cast<uint32_t *>(w + L.base),
+        reinterpret_cast<float *>(w + L.coef), counter);
+    LAUNCHCHK();
+    k.mtab = 1;
+    k.log2n = log2n;
+    return PSS_OK;
+}
+
+template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typename RF, typename RI,
+          int TRF>
+static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
     using PC = PairCols<N1, B, T, CF, CI>;
     using PR = PairRows<N2, TR, RF, RI>;
     k.poff = k.p.chan0 & 1;
     k.npairs = (k.p.nchan + k.poff + 1) / 2;
     char *w = reinterpret_cast<char *>(k.p.work);
-    k.Yd = reinterpret_cast<cf *>(w);
-    k.Ym = reinterpret_cast<cf *>(w + (int64_t)k.npairs * k.N * 8);
-    cf *mspec = reinterpret_cast<cf *>(w + (int64_t)2 * k.npairs * k.N * 8);
-    k.Mspec = mspec;
+    const WsLayout L = ws_layout(k.p.nchan, k.N);
+    k.Yd = reinterpret_cast<cf *>(w + L.yd);
     if (k.p.null_mode == PSS_NULL_DELAYED) {
-        // spectrum of the (channel independent) mask row, once per run
-        KP km = k;
-        km.p.nchan = 1;
-        km.p.chan0 = 0;
-        km.p.data = mask_row;
-        km.p.ld = k.N;
-        km.p.src = PSS_SRC_LOAD;
-        km.p.null_mode = PSS_NULL_NONE;
-        km.p.data_in_fft = 1;
-        km.p.work = mspec;
-        using C1 = Cols<N1, B, T, CF, CI>;
-        using R1 = Rows<N2, 1, TRF, RF, RI, true>;
-        k_colA<C1, T><<<dim3((unsigned)(N2 / B), 1), dim3(T), 0, st>>>(km);
-        LAUNCHCHK();
-        k_row<R1, TRF><<<dim3((unsigned)N1, 1), dim3(TRF), 0, st>>>(km);
-        LAUNCHCHK();
+        const int rc = build_mask_table<N1, B, T, CF, CI, N2, TR, RF, RI, TRF>(k, st, mask_row, w, L);
+        if (rc) return rc;
     }
-    dim3 gc((unsigned)(N2 / B), (unsigned)k.npairs);
-    if (k.p.data_in_fft) {
-        tk_begin(TK_COLA, st);
-        k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
+    if (!k.p.data_in_fft) {
+        // only the null mask was delayed: one elementwise pass with table lookups
+        dim3 g = stream_grid((k.N + 3) / 4, k.p.nchan);
+        tk_begin(TK_ELEM, st);
+        k_elementwise<<<g, dim3(256), 0, st>>>(k);
         tk_end(st);
         LAUNCHCHK();
+        return PSS_OK;
     }
+    dim3 gc((unsigned)(N2 / B), (unsigned)k.npairs);
+    tk_begin(TK_COLA, st);
+    k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
+    tk_end(st);
+    LAUNCHCHK();
     tk_begin(TK_ROW, st);
     k_pair_row<PR, TR><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
     tk_end(st);
@@ -1121,7 +1380,7 @@ static int launch_pair(KP &k, hipStream_t st, float *mask_row) {
     return PSS_OK;
 }
 
-static int run_fourstep(KP &k, hipStream_t st, float *mask_row) {
+static int run_fourstep(KP &k, hipStream_t st, const float *mask_row) {
     const int64_t N = k.N;
     if (N >= (1 << 17)) {
         k.N2 = 8192;
@@ -1217,6 +1476,8 @@ static int validate(const PssPipeline *p) {
         if (!p->work) return fail(PSS_EINVAL, "shift needs a workspace");
         if (p->nsamp > (1ll << 24) && !is_pow2(p->nsamp))
             return fail(PSS_EUNSUPPORTED, "N=%lld", (long long)p->nsamp);
+        if (p->null_mode == PSS_NULL_DELAYED && fourstep_len(p->nsamp) && !p->mask_ramp)
+            return fail(PSS_EINVAL, "delayed null needs mask_ramp");
     }
     if (p->out_kind != PSS_OUT_NONE && !p->out) return fail(PSS_EINVAL, "out is NULL");
     return PSS_OK;
@@ -1253,17 +1514,9 @@ int pss_last_error(char *buf, size_t n) {
     return (int)strlen(g_err);
 }
 
-// Layout: [spill area][mask row: nsamp floats, 256-B aligned]
-static int64_t spill_bytes(int32_t nchan, int64_t nsamp) {
-    const int64_t one = (int64_t)nchan * nsamp * 8;
-    const int64_t npairs = (nchan + 2) / 2;   // pairs of (even, odd) global channels
-    if (is_pow2(nsamp) && nsamp >= 64 && nsamp <= (1ll << 24))
-        return nsamp > 8192 ? 2 * npairs * nsamp * 8 + nsamp * 8 : 0;   // Yd, Ym, Mspec
-    return 2 * one + nsamp * 8;   // fallback: W1, W2 and the twiddle table
-}
-
 int64_t pss_workspace_bytes(int32_t nchan, int64_t nsamp) {
-    return ((spill_bytes(nchan, nsamp) + 255) & ~255ll) + nsamp * 4;
+    if (nchan <= 0 || nsamp <= 0) return 0;
+    return ws_layout(nchan, nsamp).total;
 }
 
 int pss_run(const PssPipeline *p, void *stream) {
@@ -1271,6 +1524,7 @@ int pss_run(const PssPipeline *p, void *stream) {
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
     KP k;
+    memset(&k, 0, sizeof(k));
     k.p = *p;
     k.N = p->nsamp;
     k.N1 = 1;
@@ -1286,8 +1540,7 @@ int pss_run(const PssPipeline *p, void *stream) {
         return PSS_OK;
     }
     const int64_t N = p->nsamp;
-    float *row = reinterpret_cast<float *>(reinterpret_cast<char *>(p->work) +
-                                           ((spill_bytes(p->nchan, N) + 255) & ~255ll));
+    float *row = reinterpret_cast<float *>(reinterpret_cast<char *>(p->work) + ws_layout(p->nchan, N).row);
     if (p->null_mode == PSS_NULL_DELAYED) {
         if (!p->inj_box) {
             k_box_row<<<stream_grid(N, 1), dim3(256), 0, st>>>(k, row);
