@@ -144,13 +144,19 @@ typedef struct PssPipeline {
 
 /* Library / device info. */
 int pss_version(void);
+
+/* Engine flags (test hook; returns the previous flags).  PSS_FLAG_NO_FAST
+ * routes every run through the generic kernels instead of the fast-path
+ * specialisations (which must give bitwise identical results). */
+#define PSS_FLAG_NO_FAST 1
+int pss_set_flags(int flags);
 int pss_last_error(char *buf, size_t n);
 
 /* Opt-in kernel timing for benchmarks: while enabled, pss_run records a pair
  * of hipEvents on its stream around every kernel it launches.  collect()
  * synchronises on them and returns, per launch (up to `cap`), the kernel kind
  * (0 elementwise, 1 single pass, 2 four-step column pass A, 3 row pass B,
- * 4 column pass C, 5 fallback), its milliseconds and the channel-samples it
+ * 4 column pass C, 5 fallback, 6 delayed-null fix-up), its milliseconds and the channel-samples it
  * processed; returns the number of launches reported and resets. */
 void pss_timing_enable(int on);
 int pss_timing_collect(int32_t *kind, double *ms, int64_t *units, int cap);

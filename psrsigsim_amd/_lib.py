@@ -15,9 +15,10 @@ PSS_OK, PSS_EINVAL, PSS_EUNSUPPORTED, PSS_EHIP = 0, -1, -2, -3
 SRC_LOAD, SRC_SEARCH, SRC_FOLD = 0, 1, 2
 NULL_NONE, NULL_UNDELAYED, NULL_DELAYED = 0, 1, 2
 OUT_NONE, OUT_F32, OUT_I8 = 0, 1, 2
+FLAG_NO_FAST = 1
 P_PULSE, P_BOX, P_REP, P_NOISE, P_TEST = 1, 2, 3, 4, 5
 KERNEL_KINDS = ("elementwise", "single_pass", "fourstep_colA", "fourstep_row", "fourstep_colC",
-                "fallback_dft")
+                "fallback_dft", "null_fix")
 
 c_i32, c_i64, c_u32, c_u64, c_f32, c_vp = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
                                            ctypes.c_uint64, ctypes.c_float, ctypes.c_void_p)
@@ -45,6 +46,7 @@ class PssPipeline(ctypes.Structure):
 
 EXPORTS = {
     "pss_version": (ctypes.c_int, []),
+    "pss_set_flags": (ctypes.c_int, [ctypes.c_int]),
     "pss_last_error": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
     "pss_workspace_bytes": (c_i64, [c_i32, c_i64]),
     "pss_timing_enable": (None, [ctypes.c_int]),

@@ -24,6 +24,16 @@
 #define PSS_ABLATE 0
 #endif
 static constexpr int kAbl = PSS_ABLATE;
+// Layout experiments (tools/ablate.sh): XCD-aware column-block order, and the
+// 1024 x 4096 four-step split for N = 2^22 instead of 512 x 8192.
+#ifndef PSS_XCD_MAP
+#define PSS_XCD_MAP 1
+#endif
+#ifndef PSS_SPLIT4K
+#define PSS_SPLIT4K 0
+#endif
+static constexpr bool kXcdMap = PSS_XCD_MAP != 0;
+static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 
 using namespace pss;
 
@@ -58,7 +68,7 @@ static int fail(int code, const char *fmt, ...) {
 // opt-in per-kernel timing (bench.py): hipEvents recorded on the launch stream
 // around every kernel of pss_run, summed per kernel kind on collect.
 // ---------------------------------------------------------------------------
-enum { TK_ELEM = 0, TK_SINGLE, TK_COLA, TK_ROW, TK_COLC, TK_FALLBACK, TK_N };
+enum { TK_ELEM = 0, TK_SINGLE, TK_COLA, TK_ROW, TK_COLC, TK_FALLBACK, TK_NULLFIX, TK_N };
 static bool g_timing = false;
 struct TimedLaunch { int kind; int64_t units; hipEvent_t a, b; };
 static TimedLaunch g_tl[4096];
@@ -73,12 +83,12 @@ static void tk_begin(int kind, hipStream_t st) {
     if (hipEventCreate(&t.a) != hipSuccess || hipEventCreate(&t.b) != hipSuccess) { g_tk_pending = -1; return; }
     t.kind = kind;
     t.units = g_tk_units;
-    hipEventRecord(t.a, st);
+    (void)hipEventRecord(t.a, st);
     g_tk_pending = kind;
 }
 static void tk_end(hipStream_t st) {
     if (g_tk_pending < 0) return;
-    hipEventRecord(g_tl[g_ntl].b, st);
+    (void)hipEventRecord(g_tl[g_ntl].b, st);
     ++g_ntl;
     g_tk_pending = -1;
 }
@@ -101,9 +111,11 @@ struct KP {
     // delayed-null mask table (four-step lengths; see k_mask_table)
     int mtab;               // 1: mask decisions come from the table
     int log2n;
-    const uint4 *mt_bits;   // [N/64] {ambiguous bits lo/hi, nulled bits lo/hi}
-    const uint32_t *mt_base;// [N/64] index of the block's first ambiguous position
-    const float *mt_coef;   // [n_ambiguous][KCH] Chebyshev coefficients in t
+    const uint2 *mt_bits;   // [N/32] {nulled-for-every-f bits, f-dependent bits}
+    const uint32_t *mt_base;// [N/32] index of the word's first f-dependent position
+    const float *mt_coef;   // [n_f_dependent][KCH] Chebyshev coefficients in t
+    const uint32_t *mbits;  // [nchan][N/32] per-channel null decisions (k_mask_bits)
+    int mbB;                // column-block width B of pass C (mbits layout)
 };
 
 // ---------------------------------------------------------------------------
@@ -151,31 +163,146 @@ __device__ __forceinline__ float cheb_eval(const float *c, float t) {
 }
 
 // Null decision bits (bit i: sample n0 + i) for 4 consecutive samples of a
-// channel with mask split (ishift, t).
+// channel with mask split (ishift, t): a 4-bit window of the two table words
+// covering positions p0..p0+3 (mod N), branch-free; the Chebyshev evaluation
+// only where a position's decision depends on f (~2% of positions).
 __device__ __forceinline__ uint32_t mask_hits4(const KP &k, int64_t n0, uint32_t ishift, float t) {
     const uint32_t nm = (uint32_t)k.N - 1u;
     const uint32_t p0 = ((uint32_t)n0 - ishift) & nm;
-    const uint32_t w0 = p0 >> 6, w3 = ((p0 + 3u) & nm) >> 6;
-    const uint4 W0 = k.mt_bits[w0];
-    const uint4 W3 = (w3 == w0) ? W0 : k.mt_bits[w3];
-    if (((W0.x | W0.y | W0.z | W0.w) | (W3.x | W3.y | W3.z | W3.w)) == 0u) return 0u;
-    uint32_t r = 0;
+    const uint32_t w = p0 >> 5, w2 = (w + 1u) & (nm >> 5), sh = p0 & 31u;
+    const uint2 A = k.mt_bits[w], Bw = k.mt_bits[w2];
+    uint32_t r = (uint32_t)(((((uint64_t)Bw.x) << 32) | A.x) >> sh) & 15u;
+    const uint32_t amb = (uint32_t)(((((uint64_t)Bw.y) << 32) | A.y) >> sh) & 15u;
+    if (amb) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t p = (p0 + (uint32_t)i) & nm;
-        const bool first = (p >> 6) == w0;
-        const uint4 W = first ? W0 : W3;
-        const uint32_t b = p & 63u;
-        const uint64_t amb = ((uint64_t)W.y << 32) | W.x;
-        const uint64_t hi = ((uint64_t)W.w << 32) | W.z;
-        bool hit = (hi >> b) & 1u;
-        if ((amb >> b) & 1u) {
-            const uint32_t idx = k.mt_base[p >> 6] + (uint32_t)__popcll(amb & ((1ull << b) - 1ull));
-            hit = cheb_eval(k.mt_coef + (int64_t)idx * KCH, t) > 1.0f;
+        for (int i = 0; i < 4; ++i) {
+            if ((amb >> i) & 1u) {
+                const uint32_t p = (p0 + (uint32_t)i) & nm, pw = p >> 5;
+                const uint32_t word = (pw == w) ? A.y : Bw.y;
+                const uint32_t idx = k.mt_base[pw] + (uint32_t)__popc(word & ((1u << (p & 31u)) - 1u));
+                const bool hit = cheb_eval(k.mt_coef + (int64_t)idx * KCH, t) > 1.0f;
+                r = (r & ~(1u << i)) | ((uint32_t)hit << i);
+            }
         }
-        r |= (uint32_t)hit << i;
     }
     return r;
+}
+
+// Null decisions of the RUN <= 32 contiguous samples n .. n + RUN - 1 of a
+// channel with mask split (is, t): a window of the two table words covering
+// them; the Chebyshev evaluation only at f-dependent positions (~2%).
+__device__ __forceinline__ uint32_t mask_run(const KP &k, uint32_t n, uint32_t is, float t, uint32_t RUN) {
+    const uint32_t nm = (uint32_t)k.N - 1u, wm = nm >> 5;
+    const uint32_t p0 = (n - is) & nm, w = p0 >> 5, w2 = (w + 1u) & wm, sh = p0 & 31u;
+    const uint2 A = k.mt_bits[w], Bw = k.mt_bits[w2];
+    const uint32_t msk = RUN >= 32u ? 0xffffffffu : ((1u << RUN) - 1u);
+    uint32_t r32 = (uint32_t)(((((uint64_t)Bw.x) << 32) | A.x) >> sh) & msk;
+    uint32_t amb = (uint32_t)(((((uint64_t)Bw.y) << 32) | A.y) >> sh) & msk;
+    while (amb) {
+        const uint32_t i = (uint32_t)__ffs(amb) - 1u;
+        amb &= amb - 1u;
+        const uint32_t p = (p0 + i) & nm, pw = p >> 5;
+        const uint32_t word = (pw == w) ? A.y : Bw.y;
+        const uint32_t idx = k.mt_base[pw] + (uint32_t)__popc(word & ((1u << (p & 31u)) - 1u));
+        const bool hit = cheb_eval(k.mt_coef + (int64_t)idx * KCH, t) > 1.0f;
+        r32 = (r32 & ~(1u << i)) | ((uint32_t)hit << i);
+    }
+    return r32;
+}
+
+// Per-channel null decisions for the four-step column pass C.  A pass-C
+// workgroup owns the B columns [n20, n20 + B) of every row n1 (samples
+// n1 N2 + n20 + b); looking the table up there means scattered loads 8192
+// samples apart.  k_mask_bits resolves the table once per channel into one bit
+// per sample, laid out in pass-C order: entry (n20 / B, n1) holds B bits
+// (B % 4 == 0), entries in a bit stream [chan][N2 / B][N1][B], so a workgroup
+// reads its decisions as one contiguous N1 * B-bit run per channel.
+__global__ __launch_bounds__(256) void k_mask_bits(KP k, uint32_t *bm) {
+    const int r = blockIdx.y;
+    const uint32_t j = blockIdx.x * 256u + threadIdx.x;          // output word of channel r
+    const uint32_t wm = ((uint32_t)k.N - 1u) >> 5;
+    if (j > wm) return;
+    uint32_t is;
+    float t;
+    mask_split((uint64_t)k.p.mask_ramp[r], k.log2n, is, t);
+    const uint32_t B = (uint32_t)k.mbB, RUN = B < 32u ? B : 32u;
+    const uint32_t N1 = (uint32_t)k.N1, N2 = (uint32_t)k.N2;
+    uint32_t out = 0;
+    for (uint32_t s = 0; s < 32u; s += RUN) {          // runs of RUN contiguous samples
+        const uint32_t bp = (j << 5) + s, e = bp / B, b = bp - e * B;
+        const uint32_t n = (e % N1) * N2 + (e / N1) * B + b;
+        out |= mask_run(k, n, is, t, RUN) << s;
+    }
+    bm[(int64_t)r * (wm + 1u) + j] = out;
+}
+
+// Delayed null on the fast path (see passC_fast): after pass C stored every
+// sample as signal + noise, rewrite the nulled ones as replacement + noise --
+// the same Philox draws and expression as epilogue4, so the result is bitwise
+// that of the generic kernels.  One thread per 32-sample word, natural order:
+// ~90% of the words have no nulled sample and only read two table words.  A
+// nulled pulse covers ~8 words, so the nulled 4-sample groups of a wave are
+// listed in LDS first and then drawn 64 at a time (one Philox pair per lane
+// per round) instead of up to 8 rounds in the lanes that hold them.
+__global__ __launch_bounds__(256) void k_null_fix(KP k) {
+    __shared__ uint32_t desc[4][64 * 8];
+    const int r = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+    const PssPipeline &p = k.p;
+    uint32_t is;
+    float t;
+    mask_split((uint64_t)p.mask_ramp[r], k.log2n, is, t);
+    const uint32_t hits = (j <= (((uint32_t)k.N - 1u) >> 5)) ? mask_run(k, j << 5, is, t, 32u) : 0u;
+    if (__ballot(hits != 0u) == 0ull) return;                     // wave-uniform
+    // entry = source lane << 8 | group << 4 | 4-bit decisions
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t total = 0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        const uint32_t h = (hits >> (4 * g)) & 15u;
+        const uint64_t bal = __ballot(h != 0u);
+        if (h) desc[wv][total + (uint32_t)__popcll(bal & below)] = ((uint32_t)lane << 8) | ((uint32_t)g << 4) | h;
+        total += (uint32_t)__popcll(bal);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t c = (uint32_t)(p.chan0 + r);
+    float *row = p.data + (int64_t)r * p.ld;
+    const Rng gn(p.seed, p.call_noise, P_NOISE), gr(p.seed, p.call_null, P_REP);
+    const float nn = p.noise_norm, sc = p.null_rep_scale;
+    for (uint32_t e = (uint32_t)lane; e < total; e += 64u) {
+        const uint32_t d = desc[wv][e], h = d & 15u;
+        const int64_t n = ((int64_t)(j - (uint32_t)lane + (d >> 8)) << 5) + 4 * ((d >> 4) & 15u);
+        const float4 xn = chi2_1x4(gn.bits((uint32_t)(n >> 2), c, (uint32_t)(n >> 34)));
+        const float4 xr = chi2_1x4(gr.bits((uint32_t)(n >> 2), c, (uint32_t)(n >> 34)));
+        const float vn[4] = {xn.x, xn.y, xn.z, xn.w}, vr[4] = {xr.x, xr.y, xr.z, xr.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if ((h >> i) & 1u) row[n + i] = fmaf(nn, vn[i], vr[i] * sc);
+    }
+}
+
+// 4 null decisions of channel row r for samples n1 N2 + n20 + b4 .. + 3.
+// (column block blockIdx.x of B columns, N1 rows; B, N1 as in pass C)
+template <int B, int N1>
+__device__ __forceinline__ uint32_t mask_bits4(const KP &k, int r, int cbx, int n1, int b4) {
+    const uint32_t bp = (((uint32_t)cbx * (uint32_t)N1 + (uint32_t)n1) * (uint32_t)B) + (uint32_t)b4;
+    return (k.mbits[(int64_t)r * (k.N >> 5) + (bp >> 5)] >> (bp & 31u)) & 15u;
+}
+
+// XCD-aware block order of the column passes.  Workgroups are dispatched
+// round-robin over the 8 XCDs (linear id % 8), each with its own L2; the
+// passes touch B-column segments of every row (64 B of fp32 output for B = 16,
+// half a 128-B line).  Remapping linear id -> (id % 8) * (total / 8) + id / 8
+// gives each XCD a contiguous range of column blocks, so the two halves of a
+// line are written through the same L2 at about the same time.
+__device__ __forceinline__ void xcd_block(int &bx, int &by) {
+    const uint32_t gx = gridDim.x, total = gx * gridDim.y;
+    const uint32_t id = blockIdx.x + blockIdx.y * gx;
+    const uint32_t l = (kXcdMap && (total & 7u) == 0u) ? (id & 7u) * (total >> 3) + (id >> 3) : id;
+    by = (int)(l / gx);
+    bx = (int)(l - (uint32_t)by * gx);
 }
 
 __device__ __forceinline__ int64_t floordiv(int64_t a, int64_t b) {
@@ -826,26 +953,45 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
     static constexpr int ITEMS = N1 * B / 4 / T;
     static_assert(ITEMS * 4 * T == N1 * B, "items per thread");
 
-    // A: generate channels a, b into z = d_a + i d_b; column FFTs; twiddle; spill
+    // A: generate channels a, b into z = d_a + i d_b; column FFTs; twiddle; spill.
+    // FAST (host-selected): search-mode source with Philox chi2(1) draws, no
+    // injected draws, no undelayed null -- the same values as source4.
+    template <bool FAST>
     __device__ static void passA(const KP &k) {
         __shared__ cf lds[B * Lds<N1>::RS];
         const int tid = threadIdx.x;
-        const int pr = blockIdx.y;
+        int cbx, pr;
+        xcd_block(cbx, pr);
         const int ra = 2 * pr - k.poff, rb = ra + 1;
         const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
-        const int64_t n20 = (int64_t)blockIdx.x * B;
+        const int64_t n20 = (int64_t)cbx * B;
         const int64_t N2 = k.N2;
+        const PssPipeline &p = k.p;
+        const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
+        const int pra = (p.prof_rows == 1) ? 0 : (int)ca, prb = (p.prof_rows == 1) ? 0 : (int)cb;
+        const Rng g(p.seed, p.call_gen, P_PULSE);
         for (int it = tid; it < N1 * B / 4; it += T) {
             const int n1 = it / (B / 4);
             const int b4 = (it - n1 * (B / 4)) * 4;
             const int64_t n = n1 * N2 + n20 + b4;
             float xa[4], xb[4], dum[4];
+            if constexpr (FAST) {
+                const float4 qa = chi2_1x4(g.bits((uint32_t)(n >> 2), ca, (uint32_t)(n >> 34)));
+                const float4 qb = chi2_1x4(g.bits((uint32_t)(n >> 2), cb, (uint32_t)(n >> 34)));
+                const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    xa[i] = hasa ? pchip_eval(k, pra, n + i) * va[i] * p.draw_norm : 0.f;
+                    xb[i] = hasb ? pchip_eval(k, prb, n + i) * vb[i] * p.draw_norm : 0.f;
+                }
+            } else {
             if (kAbl & 1) { for (int q = 0; q < 4; ++q) xa[q] = (float)(n + q); } else
             if (hasa) source4(k, ra, n, 4, xa, dum, true, false);
             else { xa[0] = xa[1] = xa[2] = xa[3] = 0.f; }
             if (kAbl & 1) { for (int q = 0; q < 4; ++q) xb[q] = (float)(n - q); } else
             if (hasb) source4(k, rb, n, 4, xb, dum, true, false);
             else { xb[0] = xb[1] = xb[2] = xb[3] = 0.f; }
+            }
 #pragma unroll
             for (int i = 0; i < 4; ++i) lds[Lds<N1>::at(b4 + i, n1)] = make_float2(xa[i], xb[i]);
         }
@@ -912,18 +1058,13 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
     __device__ static void passC(const KP &k) {
         __shared__ cf lds[B * Lds<N1>::RS];
         const int tid = threadIdx.x;
-        const int pr = blockIdx.y;
+        int cbx, pr;
+        xcd_block(cbx, pr);
         const int ra = 2 * pr - k.poff, rb = ra + 1;
         const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
-        const int64_t n20 = (int64_t)blockIdx.x * B;
+        const int64_t n20 = (int64_t)cbx * B;
         const bool mask = k.mtab != 0;
         const float invN = k.invN;
-        uint32_t isa = 0, isb = 0;
-        float ta = 0.f, tb = 0.f;
-        if (mask) {
-            if (hasa) mask_split((uint64_t)k.p.mask_ramp[ra], k.log2n, isa, ta);
-            if (hasb) mask_split((uint64_t)k.p.mask_ramp[rb], k.log2n, isb, tb);
-        }
         inv_block(k, k.Yd + (int64_t)pr * k.N, n20, lds, tid);
 #pragma unroll 1
         for (int t = 0; t < ITEMS; ++t) {
@@ -932,8 +1073,8 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
             const int b4 = (it - n1 * (B / 4)) * 4;
             const int64_t n = n1 * k.N2 + n20 + b4;
             float da[4], db[4], ma[4], mb[4];
-            const uint32_t ha = (mask && hasa) ? mask_hits4(k, n, isa, ta) : 0u;
-            const uint32_t hb = (mask && hasb) ? mask_hits4(k, n, isb, tb) : 0u;
+            const uint32_t ha = (mask && hasa) ? mask_bits4<B, N1>(k, ra, cbx, n1, b4) : 0u;
+            const uint32_t hb = (mask && hasb) ? mask_bits4<B, N1>(k, rb, cbx, n1, b4) : 0u;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const cf z = lds[Lds<N1>::at(b4 + i, n1)];
@@ -948,13 +1089,65 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         }
     }
 
+    // C, fast path (host-selected: Philox draws with df = 1 for noise and
+    // null replacement, no injected draws, no observe() copy).  Bitwise equal
+    // to passC.  Every sample is stored as signal + noise; the nulled samples
+    // of a delayed null are rewritten afterwards by k_null_fix (~10% of the
+    // samples; scattered 8192 apart in this kernel's column order).
+    __device__ static void passC_fast(const KP &k) {
+        __shared__ __align__(16) cf lds[B * Lds<N1>::RS];
+        const int tid = threadIdx.x;
+        int cbx, pr;
+        xcd_block(cbx, pr);
+        const int ra = 2 * pr - k.poff, rb = ra + 1;
+        const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
+        const int64_t n20 = (int64_t)cbx * B;
+        const int64_t N2 = k.N2;
+        const PssPipeline &p = k.p;
+        const float invN = k.invN, nn = p.noise_norm;
+        const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
+        inv_block(k, k.Yd + (int64_t)pr * k.N, n20, lds, tid);
+        const Rng gn(p.seed, p.call_noise, P_NOISE);
+        float acc[ITEMS][2][4];
+#pragma unroll
+        for (int t = 0; t < ITEMS; ++t) {
+            const int it = tid + t * T;
+            const int n1 = it / (B / 4);
+            const int b4 = (it - n1 * (B / 4)) * 4;
+            const int64_t n = n1 * N2 + n20 + b4;
+            const float4 xa = chi2_1x4(gn.bits((uint32_t)(n >> 2), ca, (uint32_t)(n >> 34)));
+            const float4 xb = chi2_1x4(gn.bits((uint32_t)(n >> 2), cb, (uint32_t)(n >> 34)));
+            const float na[4] = {xa.x, xa.y, xa.z, xa.w}, nb[4] = {xb.x, xb.y, xb.z, xb.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const cf z = lds[Lds<N1>::at(b4 + i, n1)];
+                acc[t][0][i] = fmaf(nn, na[i], z.x * invN);
+                acc[t][1][i] = fmaf(nn, nb[i], z.y * invN);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < ITEMS; ++t) {
+            const int it = tid + t * T;
+            const int n1 = it / (B / 4);
+            const int b4 = (it - n1 * (B / 4)) * 4;
+            const int64_t n = n1 * N2 + n20 + b4;
+            if (hasa)
+                *reinterpret_cast<float4 *>(p.data + (int64_t)ra * p.ld + n) =
+                    make_float4(acc[t][0][0], acc[t][0][1], acc[t][0][2], acc[t][0][3]);
+            if (hasb)
+                *reinterpret_cast<float4 *>(p.data + (int64_t)rb * p.ld + n) =
+                    make_float4(acc[t][1][0], acc[t][1][1], acc[t][1][2], acc[t][1][3]);
+        }
+    }
+
     // Mask table build: inverse column FFTs of node pair `blockIdx.y`, stored
     // (scaled) as node rows nodes[2 pr], nodes[2 pr + 1].
     __device__ static void node_col(const KP &k, float *nodes) {
         __shared__ cf lds[B * Lds<N1>::RS];
         const int tid = threadIdx.x;
-        const int pr = blockIdx.y;
-        const int64_t n20 = (int64_t)blockIdx.x * B;
+        int cbx, pr;
+        xcd_block(cbx, pr);
+        const int64_t n20 = (int64_t)cbx * B;
         const float invN = k.invN;
         inv_block(k, k.Ym + (int64_t)pr * k.N, n20, lds, tid);
         float *ra = nodes + (int64_t)(2 * pr) * k.N, *rb = ra + k.N;
@@ -976,9 +1169,13 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
 };
 
 template <typename C, int T>
-__global__ __launch_bounds__(T) void k_pairA(KP k) { C::passA(k); }
+__global__ __launch_bounds__(T) void k_pairA(KP k) { C::template passA<false>(k); }
+template <typename C, int T>
+__global__ __launch_bounds__(T) void k_pairA_fast(KP k) { C::template passA<true>(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairC(KP k) { C::passC(k); }
+template <typename C, int T>
+__global__ __launch_bounds__(T) void k_pairC_fast(KP k) { C::passC_fast(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_node_col(KP k, float *nodes) { C::node_col(k, nodes); }
 
@@ -999,7 +1196,7 @@ __global__ void k_node_params(uint64_t *ramp, float *nyq, int L) {
 // |M - c0| <= sum_{n>=1} |c_n| on t in [-1, 1], and compaction of the
 // coefficients of the f-dependent positions (wave ballot + one atomic per
 // wave; positions are self-describing, so the atomic order does not matter).
-__global__ __launch_bounds__(256) void k_mask_table(const float *nodes, int64_t N, uint4 *bits,
+__global__ __launch_bounds__(256) void k_mask_table(const float *nodes, int64_t N, uint2 *bits,
                                                     uint32_t *base, float *coef, uint32_t *counter) {
     __shared__ float T[KCH * KCH];
     if (threadIdx.x < KCH * KCH) {
@@ -1029,9 +1226,11 @@ __global__ __launch_bounds__(256) void k_mask_table(const float *nodes, int64_t 
     uint32_t b0 = 0;
     if (lane == 0 && ab) b0 = atomicAdd(counter, (uint32_t)__popcll(ab));
     b0 = __shfl(b0, 0);
-    if (lane == 0) {
-        bits[p >> 6] = make_uint4((uint32_t)ab, (uint32_t)(ab >> 32), (uint32_t)hb, (uint32_t)(hb >> 32));
-        base[p >> 6] = b0;
+    if (lane == 0) {   // this wave's 64 positions = table words p/32, p/32 + 1
+        bits[p >> 5] = make_uint2((uint32_t)hb, (uint32_t)ab);
+        bits[(p >> 5) + 1] = make_uint2((uint32_t)(hb >> 32), (uint32_t)(ab >> 32));
+        base[p >> 5] = b0;
+        base[(p >> 5) + 1] = b0 + (uint32_t)__popc((uint32_t)ab);
     }
     if (amb) {
         const uint32_t idx = b0 + (uint32_t)__popcll(ab & ((1ull << lane) - 1ull));
@@ -1245,7 +1444,8 @@ using C8kI = RList<8, 8, 8, 16>;
 //   four-step (N = 2^m, 2^14 <= N <= 2^24):
 //     Yd [npairs][N] cf | Mspec [N] cf | node spill [KCH/2][N] cf |
 //     nodes [KCH][N] f32 | table bits [N/64] uint4 | base [N/64] u32 |
-//     coef [N][KCH] f32 (worst case) | misc (counter, node ramps/nyq) | mask row [N] f32
+//     coef [N][KCH] f32 (worst case) | misc (counter, node ramps/nyq) |
+//     null bits [nchan][N/32] u32 | mask row [N] f32
 //   single pass (N <= 8192): mask row
 //   direct DFT fallback: W1, W2 [nchan][N] cf | twiddles [N] cf | mask row
 // ---------------------------------------------------------------------------
@@ -1253,7 +1453,7 @@ static inline int64_t al256(int64_t b) { return (b + 255) & ~255ll; }
 static inline bool fourstep_len(int64_t n) { return is_pow2(n) && n >= 16384 && n <= (1ll << 24); }
 
 struct WsLayout {
-    int64_t yd, mspec, ynode, nodes, bits, base, coef, misc, row, total;
+    int64_t yd, mspec, ynode, nodes, bits, base, coef, misc, mbits, row, total;
 };
 
 static WsLayout ws_layout(int32_t nchan, int64_t N) {
@@ -1266,10 +1466,11 @@ static WsLayout ws_layout(int32_t nchan, int64_t N) {
         w.mspec = o; o += al256(N * 8);
         w.ynode = o; o += al256((int64_t)(KCH / 2) * N * 8);
         w.nodes = o; o += al256((int64_t)KCH * N * 4);
-        w.bits = o;  o += al256((N / 64) * 16);
-        w.base = o;  o += al256((N / 64) * 4);
+        w.bits = o;  o += al256((N / 32) * 8);
+        w.base = o;  o += al256((N / 32) * 4);
         w.coef = o;  o += al256(N * KCH * 4);
         w.misc = o;  o += 256;
+        w.mbits = o; o += al256((int64_t)nchan * (N / 8));   // per-channel null bits
     } else if (!(is_pow2(N) && N >= 64 && N <= 8192)) {
         o += al256(2 * (int64_t)nchan * N * 8 + N * 8);    // fallback: W1, W2, twiddles
     }
@@ -1277,6 +1478,24 @@ static WsLayout ws_layout(int32_t nchan, int64_t N) {
     o += al256(N * 4);
     w.total = o;
     return w;
+}
+
+// Fast-path selection (kernels specialised for the north-star configuration;
+// results are bitwise identical to the generic kernels).
+static int g_flags = 0;   // pss_set_flags (test hook)
+
+static bool fast_source(const PssPipeline &p) {
+    if (g_flags & PSS_FLAG_NO_FAST) return false;
+    return p.src == PSS_SRC_SEARCH && p.gen_df == 1.0f && !p.inj_gen && p.null_mode != PSS_NULL_UNDELAYED;
+}
+static bool fast_epilogue(const KP &k) {
+    const PssPipeline &p = k.p;
+    if (g_flags & PSS_FLAG_NO_FAST) return false;
+    if (p.out_kind != PSS_OUT_NONE || p.inj_noise || p.inj_rep) return false;
+    if (!p.noise || p.noise_df != 1.0f) return false;
+    if (p.null_mode == PSS_NULL_UNDELAYED) return false;
+    if (p.null_mode == PSS_NULL_DELAYED && (!k.mtab || p.null_rep_df != 1.0f)) return false;
+    return (p.ld % 4) == 0 && (((uintptr_t)p.data) & 15) == 0;
 }
 
 // Mask table of a delayed null (see the comment above KCH): mask spectrum,
@@ -1329,15 +1548,22 @@ static int build_mask_table(KP &k, hipStream_t st, const float *mask_row, char *
     LAUNCHCHK();
     // table
     HIPCHK(hipMemsetAsync(counter, 0, 4, st));
-    k.mt_bits = reinterpret_cast<const uint4 *>(w + L.bits);
+    k.mt_bits = reinterpret_cast<const uint2 *>(w + L.bits);
     k.mt_base = reinterpret_cast<const uint32_t *>(w + L.base);
     k.mt_coef = reinterpret_cast<const float *>(w + L.coef);
     k_mask_table<<<dim3((unsigned)(k.N / 256)), dim3(256), 0, st>>>(
-        nodes, k.N, reinterpret_cast<uint4 *>(w + L.bits), reinterpret_cast<uint32_t *>(w + L.base),
+        nodes, k.N, reinterpret_cast<uint2 *>(w + L.bits), reinterpret_cast<uint32_t *>(w + L.base),
         reinterpret_cast<float *>(w + L.coef), counter);
     LAUNCHCHK();
     k.mtab = 1;
     k.log2n = log2n;
+    if (k.p.data_in_fft && !fast_epilogue(k)) {   // generic pass C reads the decisions as bits
+        k.mbB = B;
+        uint32_t *bm = reinterpret_cast<uint32_t *>(w + L.mbits);
+        k_mask_bits<<<dim3((unsigned)((k.N / 32 + 255) / 256), (unsigned)k.p.nchan), dim3(256), 0, st>>>(k, bm);
+        LAUNCHCHK();
+        k.mbits = bm;
+    }
     return PSS_OK;
 }
 
@@ -1366,22 +1592,36 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
     }
     dim3 gc((unsigned)(N2 / B), (unsigned)k.npairs);
     tk_begin(TK_COLA, st);
-    k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
+    if (fast_source(k.p)) k_pairA_fast<PC, T><<<gc, dim3(T), 0, st>>>(k);
+    else k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
     tk_end(st);
     LAUNCHCHK();
     tk_begin(TK_ROW, st);
     k_pair_row<PR, TR><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
     tk_end(st);
     LAUNCHCHK();
+    const bool fast = fast_epilogue(k);
     tk_begin(TK_COLC, st);
-    k_pairC<PC, T><<<gc, dim3(T), 0, st>>>(k);
+    if (fast) k_pairC_fast<PC, T><<<gc, dim3(T), 0, st>>>(k);
+    else k_pairC<PC, T><<<gc, dim3(T), 0, st>>>(k);
     tk_end(st);
     LAUNCHCHK();
+    if (fast && k.mtab) {
+        tk_begin(TK_NULLFIX, st);
+        k_null_fix<<<dim3((unsigned)((k.N / 32 + 255) / 256), (unsigned)k.p.nchan), dim3(256), 0, st>>>(k);
+        tk_end(st);
+        LAUNCHCHK();
+    }
     return PSS_OK;
 }
 
 static int run_fourstep(KP &k, hipStream_t st, const float *mask_row) {
     const int64_t N = k.N;
+    if (kSplit4k && N == (1 << 22)) {
+        k.N2 = 4096;
+        k.N1 = 1024;
+        return launch_pair<1024, 8, 512, C1kF, C1kF, 4096, 512, C4k, C4k, 256>(k, st, mask_row);
+    }
     if (N >= (1 << 17)) {
         k.N2 = 8192;
         k.N1 = N / 8192;
@@ -1487,6 +1727,12 @@ extern "C" {
 
 int pss_version(void) { return 100; }
 
+int pss_set_flags(int flags) {
+    const int old = g_flags;
+    g_flags = flags;
+    return old;
+}
+
 void pss_timing_enable(int on) {
     g_timing = on != 0;
 }
@@ -1496,11 +1742,11 @@ int pss_timing_collect(int32_t *kind, double *ms, int64_t *units, int cap) {
     for (int i = 0; i < g_ntl; ++i) {
         TimedLaunch &t = g_tl[i];
         float e = 0.f;
-        hipEventSynchronize(t.b);
-        hipEventElapsedTime(&e, t.a, t.b);
+        (void)hipEventSynchronize(t.b);
+        (void)hipEventElapsedTime(&e, t.a, t.b);
         if (n < cap) { kind[n] = t.kind; ms[n] = e; units[n] = t.units; ++n; }
-        hipEventDestroy(t.a);
-        hipEventDestroy(t.b);
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
     }
     g_ntl = 0;
     return n;

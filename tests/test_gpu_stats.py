@@ -65,6 +65,38 @@ def test_shard_invariance_bitwise(log2n, hip_lib):
     np.testing.assert_array_equal(np.vstack([a, b]), full)
 
 
+@pytest.mark.parametrize("nchan,log2n,null", [(3, 16, True), (4, 17, True), (5, 14, True), (2, 16, False)])
+def test_fast_path_bitwise_equals_generic(nchan, log2n, null, hip_lib):
+    """The fast-path kernels (Philox df=1, no injection: the north-star
+    configuration) against the generic kernels, bit for bit."""
+    from psrsigsim_amd import _lib
+
+    def run():
+        import psrsigsim_amd as pss
+        from psrsigsim_amd.signal import FilterBankSignal
+        from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+        from psrsigsim_amd.ism import ISM
+        from psrsigsim_amd.telescope import telescope as T
+        pss.seed(11)
+        sig = FilterBankSignal(1400, 400, Nsubband=nchan, fold=False)
+        psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
+        psr.make_pulses(sig, tobs=(1 << log2n) * 20.48e-6)
+        ISM().disperse(sig, 100)
+        if null:
+            psr.null(sig, 0.2)
+        T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True)
+        return sig.data.cpu().numpy()
+
+    L = _lib.lib()
+    fast = run()
+    old = L.pss_set_flags(_lib.FLAG_NO_FAST)
+    try:
+        generic = run()
+    finally:
+        L.pss_set_flags(old)
+    np.testing.assert_array_equal(fast, generic)
+
+
 def test_shard_invariance_odd_boundary_close(hip_lib):
     """Odd boundary: bit-for-bit only up to the pair partner's rounding."""
     full = _c3_small(8, None, 16)

@@ -8,7 +8,7 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out
 mkdir -p $OUT
 cd $R
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/gpu_tests_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/gpu_tests_$TAG.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -2 $OUT/gpu_tests_$TAG.log
 [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
 timeout -k 10 600 python bench.py "$@" > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || exit $?
