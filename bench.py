@@ -98,12 +98,13 @@ def cpu_model():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--nchan", type=int, default=NCHAN, help="channels per GPU")
     ap.add_argument("--log2n", type=int, default=LOG2N)
     ap.add_argument("--cpu-chans", type=int, default=8, help="oracle sample size (channels)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--verbose", action="store_true", help="per-step wall times on stderr")
     args = ap.parse_args()
 
     import torch
@@ -135,11 +136,19 @@ def main():
     _lib.load().pss_timing_enable(1)
     _lib.timing_collect()
     t0 = time.perf_counter()
+    marks = []
     for _ in range(args.steps):
         s = c3_step(pss, total, shard, args.log2n)
         del s
+        marks.append(time.perf_counter())
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    if args.verbose:
+        prev = t0
+        for i, m in enumerate(marks):
+            print("step %d host-return %.2f ms" % (i, (m - prev) * 1e3), file=sys.stderr)
+            prev = m
+        print("final sync %.2f ms" % ((t1 - marks[-1]) * 1e3), file=sys.stderr)
     barrier()
     _lib.load().pss_timing_enable(0)
     launches = _lib.timing_collect()

@@ -23,7 +23,9 @@ def build(force=False, verbose=True):
     if not force and not stale():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
+    # -fno-slp-vectorize: packed f32 (v_pk_*) issues at half rate on gfx950 and
+    # costs register-pair moves; scalar f32 is cheaper here.
+    cmd = [hipcc, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-slp-vectorize",
            "-I" + os.path.join(ROOT, "include"), "-o", OUT + ".tmp"] + SRC
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

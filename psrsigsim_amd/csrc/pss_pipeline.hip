@@ -30,7 +30,7 @@ static constexpr int kAbl = PSS_ABLATE;
 #define PSS_XCD_MAP 1
 #endif
 #ifndef PSS_SPLIT4K
-#define PSS_SPLIT4K 0
+#define PSS_SPLIT4K 1
 #endif
 static constexpr bool kXcdMap = PSS_XCD_MAP != 0;
 static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
@@ -935,9 +935,10 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
 };
 
 template <typename R, int T>
-__global__ __launch_bounds__(T) void k_pair_row(KP k) { R::template pass<false>(k); }
+__global__ __launch_bounds__(T, (T <= 512 ? 2 * T / 256 : 4)) void k_pair_row(KP k) { R::template pass<false>(k); }
 template <typename R, int T>
 __global__ __launch_bounds__(T) void k_node_row(KP k) { R::template pass<true>(k); }
+
 
 template <int N1, int B, int T, typename FWD, typename INV>
 struct PairCols;

@@ -87,7 +87,7 @@ def _big_case(log2n, nchan, null=True, fd=True):
 
 @pytest.mark.parametrize("fused", [True, False], ids=["fused", "staged"])
 @pytest.mark.parametrize("log2n,nchan,null", [(14, 3, True), (16, 3, True), (17, 2, True),
-                                               (17, 3, False), (20, 1, True)])
+                                               (17, 3, False), (20, 1, True), (22, 3, True)])
 def test_fourstep_pair_path_vs_oracle(log2n, nchan, null, fused, hip_lib):
     """The four-step PAIR path (odd and even channel counts, with and without
     the delayed-null mask, fused and staged = mask-only FFT) against the

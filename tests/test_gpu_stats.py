@@ -65,7 +65,8 @@ def test_shard_invariance_bitwise(log2n, hip_lib):
     np.testing.assert_array_equal(np.vstack([a, b]), full)
 
 
-@pytest.mark.parametrize("nchan,log2n,null", [(3, 16, True), (4, 17, True), (5, 14, True), (2, 16, False)])
+@pytest.mark.parametrize("nchan,log2n,null", [(3, 16, True), (4, 17, True), (5, 14, True), (2, 16, False),
+                                             (3, 22, True)])
 def test_fast_path_bitwise_equals_generic(nchan, log2n, null, hip_lib):
     """The fast-path kernels (Philox df=1, no injection: the north-star
     configuration) against the generic kernels, bit for bit."""

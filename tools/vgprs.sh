@@ -1,6 +1,6 @@
 #!/bin/bash
 # Compile the pipeline for gfx950 and list VGPRs / occupancy / scratch per kernel.
-cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c -I/root/repo/include \
+cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-slp-vectorize -c -I/root/repo/include \
   /root/repo/psrsigsim_amd/csrc/pss_pipeline.hip -o /tmp/vg.o -Rpass-analysis=kernel-resource-usage "$@" 2>&1 | \
 python3 -c '
 import sys, re
