@@ -65,8 +65,9 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
         // one v_mad_u64_u32 per product (hi and lo together), not mul_hi + mul_lo
         const uint64_t p0 = (uint64_t)c.x * 0xD2511F53u;
         const uint64_t p1 = (uint64_t)c.z * 0xCD9E8D57u;
-        c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1,
-                       (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0);
+        // three-way xors as one v_bitop3_b32 each (truth table 0x96 = a ^ b ^ c)
+        c = make_uint4(__builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c.y, k0, 0x96), (uint32_t)p1,
+                       __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c.w, k1, 0x96), (uint32_t)p0);
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }

@@ -352,7 +352,9 @@ __device__ __forceinline__ void draw4(const Rng &g, int64_t n0, uint32_t c, floa
     }
 }
 
-__device__ __forceinline__ float pchip_eval(const KP &k, int prow, int64_t n) {
+// Interval index and fraction of sample n's pulse phase (shared by every
+// channel: only the coefficient row differs).
+__device__ __forceinline__ void pchip_locate(const KP &k, int64_t n, uint32_t &iv, float &u) {
     const PssPipeline &p = k.p;
     // ph = n * phase_step mod 2^64 (2^-64 cycles), n < 2^32: 32-bit products only
     const uint32_t nn = (uint32_t)n;
@@ -361,14 +363,24 @@ __device__ __forceinline__ float pchip_eval(const KP &k, int prow, int64_t n) {
     // ph * M = iv 2^64 + fraction; u = (ph * M) >> 32 holds iv and fraction bits 32..63
     const uint64_t t = (uint64_t)(uint32_t)ph * p.knot_m;
     const uint64_t u64 = (uint64_t)(uint32_t)(ph >> 32) * p.knot_m + (t >> 32);
-    uint32_t iv = (uint32_t)(u64 >> 32);                           // interval index
-    float u = (float)((uint32_t)u64 >> 8) * 5.9604644775390625e-08f;   // fraction, 24 bits
+    iv = (uint32_t)(u64 >> 32);                                    // interval index
+    u = (float)((uint32_t)u64 >> 8) * 5.9604644775390625e-08f;     // fraction, 24 bits
     if (iv >= (uint32_t)p.nint) {                                  // extrapolate
         u += (float)(iv - (uint32_t)(p.nint - 1));
         iv = p.nint - 1;
     }
-    const float4 cc = reinterpret_cast<const float4 *>(p.prof)[(int64_t)prow * p.nint + iv];
+}
+
+__device__ __forceinline__ float pchip_row(const KP &k, int prow, uint32_t iv, float u) {
+    const float4 cc = reinterpret_cast<const float4 *>(k.p.prof)[(int64_t)prow * k.p.nint + iv];
     return fmaf(fmaf(fmaf(cc.x, u, cc.y), u, cc.z), u, cc.w);
+}
+
+__device__ __forceinline__ float pchip_eval(const KP &k, int prow, int64_t n) {
+    uint32_t iv;
+    float u;
+    pchip_locate(k, n, iv, u);
+    return pchip_row(k, prow, iv, u);
 }
 
 // Source stage for 4 consecutive samples (cnt valid) of local row r.
@@ -982,8 +994,11 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
                 const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    xa[i] = hasa ? pchip_eval(k, pra, n + i) * va[i] * p.draw_norm : 0.f;
-                    xb[i] = hasb ? pchip_eval(k, prb, n + i) * vb[i] * p.draw_norm : 0.f;
+                    uint32_t iv;
+                    float u;
+                    pchip_locate(k, n + i, iv, u);
+                    xa[i] = hasa ? pchip_row(k, pra, iv, u) * va[i] * p.draw_norm : 0.f;
+                    xb[i] = hasb ? pchip_row(k, prb, iv, u) * vb[i] * p.draw_norm : 0.f;
                 }
             } else {
             if (kAbl & 1) { for (int q = 0; q < 4; ++q) xa[q] = (float)(n + q); } else
