@@ -8,8 +8,11 @@ namespace pss {
 
 typedef float2 cf;
 
+// Explicit fused forms: with free contraction the compiler picks which product
+// to fuse per call site, so the same math rounds differently in different
+// kernels (the fast-path kernels must match the generic ones bit for bit).
 __device__ __forceinline__ cf cmul(cf a, cf b) {
-    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+    return make_float2(fmaf(a.x, b.x, -(a.y * b.y)), fmaf(a.x, b.y, a.y * b.x));
 }
 __device__ __forceinline__ cf cadd(cf a, cf b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ cf csub(cf a, cf b) { return make_float2(a.x - b.x, a.y - b.y); }
@@ -53,6 +56,22 @@ struct Buf {
         w.x = __float_as_uint(v.x);
         w.y = __float_as_uint(v.y);
         __builtin_amdgcn_raw_buffer_store_b64(w, r, voff, soff, 0);
+    }
+    // AUX = cache policy bits (gfx950: 1 = sc0, 2 = nt, 16 = sc1)
+    template <int AUX = 0>
+    __device__ __forceinline__ float4 ld4(uint32_t voff, uint32_t soff) const {
+        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+        u4 w = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX);
+        return make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
+    }
+    __device__ __forceinline__ void st4(float a, float b, float c, float d, uint32_t voff, uint32_t soff) const {
+        typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+        u4 w;
+        w.x = __float_as_uint(a);
+        w.y = __float_as_uint(b);
+        w.z = __float_as_uint(c);
+        w.w = __float_as_uint(d);
+        __builtin_amdgcn_raw_buffer_store_b128(w, r, voff, soff, 0);
     }
 };
 

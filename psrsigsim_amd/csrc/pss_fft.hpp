@@ -146,6 +146,12 @@ struct Fft {
                 constexpr int H = (R >= 8) ? R / 2 : R;   // powers kept: w^1 .. w^(H-1)
                 cf w[H];
                 const float base = (float)k * (1.0f / (float)(Ns * R));   // [0, 1/R)
+#if defined(PSS_ABLATE) && (PSS_ABLATE & 32)
+                // ablation: twiddles without generation cost (wrong values)
+#pragma unroll
+                for (int q = 1; q < R; ++q) a[q] = cmul(a[q], make_float2(base, (float)q));
+                if (true) { dft<R, INV>(a); continue; }
+#endif
 #pragma unroll
                 for (int p2 = 1; p2 < H; p2 *= 2) w[p2] = expi_rev(INV ? p2 * base : -p2 * base);
 #pragma unroll

@@ -35,6 +35,7 @@ static constexpr int kAbl = PSS_ABLATE;
 static constexpr bool kXcdMap = PSS_XCD_MAP != 0;
 static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 
+
 using namespace pss;
 
 // ---------------------------------------------------------------------------
@@ -116,6 +117,7 @@ struct KP {
     const float *mt_coef;   // [n_f_dependent][KCH] Chebyshev coefficients in t
     const uint32_t *mbits;  // [nchan][N/32] per-channel null decisions (k_mask_bits)
     int mbB;                // column-block width B of pass C (mbits layout)
+    const cf *rtab;         // [nchan][RFL] row-pass ramp factors (k_ramp_tab)
 };
 
 // ---------------------------------------------------------------------------
@@ -138,6 +140,9 @@ struct KP {
 // nothing but a table lookup remains (no per-channel mask FFT or spill).
 // ---------------------------------------------------------------------------
 static constexpr int KCH = 12;
+// PCHIP intervals the fast pass A keeps in LDS (two rows; 69.7 KB FFT buffer +
+// 12 KB still allows two 512-thread workgroups per CU).
+static constexpr int kFastNint = 376;
 
 // t = 2 f - 1 and i from the mask ramp word w = frac(s / N) 2^64 (N = 2^L)
 __device__ __forceinline__ void mask_split(uint64_t w, int L, uint32_t &ishift, float &t) {
@@ -293,10 +298,15 @@ __device__ __forceinline__ uint32_t mask_bits4(const KP &k, int r, int cbx, int 
 
 // XCD-aware block order of the column passes.  Workgroups are dispatched
 // round-robin over the 8 XCDs (linear id % 8), each with its own L2; the
-// passes touch B-column segments of every row (64 B of fp32 output for B = 16,
-// half a 128-B line).  Remapping linear id -> (id % 8) * (total / 8) + id / 8
-// gives each XCD a contiguous range of column blocks, so the two halves of a
-// line are written through the same L2 at about the same time.
+// passes touch B-column segments of every row (32 B of fp32 output per channel
+// for B = 8, a quarter of a 128-B line).  Remapping linear id ->
+// (id % 8) * (total / 8) + id / 8 gives each XCD a contiguous range of column
+// blocks, so the pieces of a line are written through the same L2 at about the
+// same time and merge there.  Measured (pass C, 2048 x 2^22): 17.8-19 ms with
+// the remap, 61 ms without, 58 ms with the blocks bit-reversed over the row;
+// contiguous (wrong-place) stores would take 14.3 ms -- the residual cost of
+// the strided output is ~4 ms.  Non-temporal / sc1 loads of the spill make it
+// worse (21-25 ms): neighbouring blocks share the spill's lines through L2.
 __device__ __forceinline__ void xcd_block(int &bx, int &by) {
     const uint32_t gx = gridDim.x, total = gx * gridDim.y;
     const uint32_t id = blockIdx.x + blockIdx.y * gx;
@@ -822,6 +832,23 @@ __device__ __forceinline__ cf ramp_q(uint64_t p0, uint64_t step, uint64_t nw, in
     return expi_rev(-fix_to_rev(ph));
 }
 
+// Per-channel factors of the row-pass ramps: bin kb0 + q N/RFL has phase
+// p0 + q (N/RFL) w - [2q >= RFL] N w; the q-dependent part is the same for every
+// thread, so it is tabulated once per run (double precision, with the 1/2 of
+// the Hermitian separation folded in) and a bin's ramp is base(kb0) * tab[q].
+template <int RFL>
+__global__ void k_ramp_tab(const uint64_t *ramp, int64_t N, int nchan, cf *tab) {
+    const int r = blockIdx.x, q = threadIdx.x;
+    if (r >= nchan || q >= RFL) return;
+    const uint64_t w = (uint64_t)ramp[r];
+    uint64_t ph = (uint64_t)q * ((uint64_t)(N / RFL) * w);
+    if (2 * q >= RFL) ph -= (uint64_t)N * w;
+    const double rev = (double)(int64_t)ph * 5.421010862427522e-20;   // 2^-64
+    double sn, cs;
+    sincospi(2.0 * rev, &sn, &cs);
+    tab[(int64_t)r * RFL + q] = make_float2((float)(0.5 * cs), (float)(-0.5 * sn));
+}
+
 template <int N2, int T, typename FWD, typename INV>
 struct PairRows;
 
@@ -875,6 +902,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                 const int row = b ? rowB : rowA;
                 const int64_t kb0 = row + (int64_t)N1 * jj;
                 const uint64_t p0a = (uint64_t)kb0 * rwa, p0b = (uint64_t)kb0 * rwb;
+                const cf ba = expi_rev(-fix_to_rev(p0a)), bb = expi_rev(-fix_to_rev(p0b));
 #pragma unroll
                 for (int q = 0; q < RFL; ++q) {
                     const int i = ib * RFL + q, k2 = jj + q * LRL;
@@ -882,17 +910,19 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                     if (j == 0) { bm = b; k2m = (row == 0) ? ((N2 - k2) & (N2 - 1)) : (N2 - 1 - k2); }
                     else        { bm = 1 - b; k2m = N2 - 1 - k2; }
                     const cf Z = v[i], Zm = lds[Lds<N2>::at(bm, k2m)];
-                    const cf Da = make_float2(0.5f * (Z.x + Zm.x), 0.5f * (Z.y - Zm.y));
-                    const cf Db = make_float2(0.5f * (Z.y + Zm.y), 0.5f * (Zm.x - Z.x));
+                    // 2 D_a and 2 D_b (the 1/2 is folded into the ramp table)
+                    const cf Sa = make_float2(Z.x + Zm.x, Z.y - Zm.y);
+                    const cf Sb = make_float2(Z.y + Zm.y, Zm.x - Z.x);
                     if constexpr (kAbl & 8) {
-                        v[i] = cadd(Da, Db);
+                        v[i] = cadd(Sa, Sb);
                     } else if (kb0 == 0 && 2 * q == RFL) {          // Nyquist bin
-                        v[i] = make_float2(Da.x * k.p.nyq_re[ra], Db.x * k.p.nyq_re[rb]);
+                        v[i] = make_float2((0.5f * Sa.x) * k.p.nyq_re[ra], (0.5f * Sb.x) * k.p.nyq_re[rb]);
                     } else if (kb0 == 0 && q == 0) {                // DC
+                        const cf Da = make_float2(0.5f * Sa.x, 0.5f * Sa.y), Db = make_float2(0.5f * Sb.x, 0.5f * Sb.y);
                         v[i] = make_float2(Da.x - Db.y, Da.y + Db.x);
                     } else {
-                        const cf A = cmul(Da, ramp_q<RFL>(p0a, sta, nwa, q));
-                        const cf Bv = cmul(Db, ramp_q<RFL>(p0b, stb, nwb, q));
+                        const cf A = cmul(Sa, cmul(ba, k.rtab[(int64_t)ra * RFL + q]));
+                        const cf Bv = cmul(Sb, cmul(bb, k.rtab[(int64_t)rb * RFL + q]));
                         v[i] = make_float2(A.x - Bv.y, A.y + Bv.x);
                     }
                 }
@@ -983,12 +1013,53 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
         const int pra = (p.prof_rows == 1) ? 0 : (int)ca, prb = (p.prof_rows == 1) ? 0 : (int)cb;
         const Rng g(p.seed, p.call_gen, P_PULSE);
+        if constexpr (FAST && !(kAbl & 1)) {
+            // The pair's two PCHIP rows are staged in LDS (host guarantees
+            // nint <= kFastNint), the items are unrolled and branch-free, so
+            // the table reads of an item issue together instead of one
+            // exposed global-load latency per sample.
+            __shared__ float4 ptab[2][kFastNint];
+            const int nint = p.nint;
+            const int last = p.prof_rows - 1;
+            const int rowa = min(max(pra, 0), last), rowb = min(max(prb, 0), last);
+            const float4 *prof = reinterpret_cast<const float4 *>(p.prof);
+            for (int i = tid; i < nint; i += T) {
+                ptab[0][i] = prof[(int64_t)rowa * nint + i];
+                ptab[1][i] = prof[(int64_t)rowb * nint + i];
+            }
+            __syncthreads();
+            const float dn = p.draw_norm;
+#pragma unroll
+            for (int t = 0; t < ITEMS; ++t) {
+                const int it = tid + t * T;
+                const int n1 = it / (B / 4);
+                const int b4 = (it - n1 * (B / 4)) * 4;
+                const uint32_t n = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4;   // N <= 2^24
+                const float4 qa = chi2_1x4(g.bits(n >> 2, ca, 0u));
+                const float4 qb = chi2_1x4(g.bits(n >> 2, cb, 0u));
+                const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    uint32_t iv;
+                    float u;
+                    pchip_locate(k, (int64_t)(n + (uint32_t)i), iv, u);
+                    const float4 A = ptab[0][iv], Bc = ptab[1][iv];
+                    const float pa = fmaf(fmaf(fmaf(A.x, u, A.y), u, A.z), u, A.w);
+                    const float pb = fmaf(fmaf(fmaf(Bc.x, u, Bc.y), u, Bc.z), u, Bc.w);
+                    const float xa = pa * va[i] * dn, xb = pb * vb[i] * dn;
+                    lds[Lds<N1>::at(b4 + i, n1)] = make_float2(hasa ? xa : 0.f, hasb ? xb : 0.f);
+                }
+            }
+        } else
         for (int it = tid; it < N1 * B / 4; it += T) {
             const int n1 = it / (B / 4);
             const int b4 = (it - n1 * (B / 4)) * 4;
             const int64_t n = n1 * N2 + n20 + b4;
             float xa[4], xb[4], dum[4];
-            if constexpr (FAST) {
+            if constexpr (FAST && (kAbl & 1)) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) { xa[i] = (float)(n + i); xb[i] = (float)(n - i); }
+            } else if constexpr (FAST) {
                 const float4 qa = chi2_1x4(g.bits((uint32_t)(n >> 2), ca, (uint32_t)(n >> 34)));
                 const float4 qb = chi2_1x4(g.bits((uint32_t)(n >> 2), cb, (uint32_t)(n >> 34)));
                 const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
@@ -997,8 +1068,13 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
                     uint32_t iv;
                     float u;
                     pchip_locate(k, n + i, iv, u);
+                    if constexpr (kAbl & 16) {   // no profile-table gather
+                        xa[i] = hasa ? u * va[i] * p.draw_norm : 0.f;
+                        xb[i] = hasb ? (u + (float)iv) * vb[i] * p.draw_norm : 0.f;
+                    } else {
                     xa[i] = hasa ? pchip_row(k, pra, iv, u) * va[i] * p.draw_norm : 0.f;
                     xb[i] = hasb ? pchip_row(k, prb, iv, u) * vb[i] * p.draw_norm : 0.f;
+                    }
                 }
             } else {
             if (kAbl & 1) { for (int q = 0; q < 4; ++q) xa[q] = (float)(n + q); } else
@@ -1021,7 +1097,8 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         for (int i = 0; i < E; ++i) {
             int b, k1;
             FF::template where<RFL>(i, tid, b, k1);
-            const int64_t m = (n20 + b) * (int64_t)k1;
+            // (n20 + b) k1 < N1 N2 = N <= 2^24: exact in 32-bit and in float
+            const uint32_t m = (uint32_t)(n20 + b) * (uint32_t)k1;
             float rev = (float)m * invN;
             if (rev >= 0.5f) rev -= 1.0f;
             if constexpr (!(kAbl & 4)) v[i] = cmul(v[i], expi_rev(-rev)); else v[i] = v[i];
@@ -1041,23 +1118,42 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
     }
 
     // inverse column FFTs of one spilled pair block; result left in LDS in
-    // natural order (Lds<N1>::at(column, n1)), unscaled
-    __device__ static void inv_block(const KP &k, const cf *Yp, int64_t n20, cf *lds, int tid) {
+    // natural order (Lds<N1>::at(column, n1)), unscaled.  The load loop is
+    // deliberately rolled: with every load of the block in flight at once
+    // (64 KB per workgroup) the column passes overflow the XCD's L2 and the
+    // half-line reads / 32-B output segments of neighbouring blocks stop
+    // merging (PMC: +19% FETCH, +31% WRITE, pass C 17.6 -> 18.5 ms).
+    __device__ static __forceinline__ void inv_block(const KP &k, const cf *Yp, int64_t n20, cf *lds, int tid) {
         const int64_t N2 = k.N2;
         const float invN = k.invN;
+        const Buf Y(Yp, (uint32_t)(N1 * N2 * 8));      // one pair spill, < 2^28 bytes
+        const uint32_t s0 = (uint32_t)n20 * 8u;        // wave-uniform part of the offset
+#pragma unroll 1
         for (int it = tid; it < N1 * B / 4; it += T) {
             const int k1 = it / (B / 4);
             const int b4 = (it - k1 * (B / 4)) * 4;
-            const float4 *src = reinterpret_cast<const float4 *>(Yp + (int64_t)k1 * N2 + n20 + b4);
-            const float4 lo = src[0], hi = src[1];
+            uint32_t off = ((uint32_t)k1 * (uint32_t)N2 + (uint32_t)b4) * 8u;
+            uint32_t so = s0;
+            if constexpr (kAbl & 128) {   // ablation: contiguous loads (wrong data)
+                off = (uint32_t)it * 32u;
+                so = (uint32_t)n20 * (uint32_t)(N1 * 8);
+            }
+            const float4 lo = Y.ld4(off, so), hi = Y.ld4(off + 16u, so);
             const cf a[4] = {make_float2(lo.x, lo.y), make_float2(lo.z, lo.w),
                              make_float2(hi.x, hi.y), make_float2(hi.z, hi.w)};
+            // W^{m}, m = (n20 + b4 + i) k1 < N (exact in 32-bit and float):
+            // W^{(n20 + b4) k1} (W^{k1})^i -- two native sincos per 4 points
+            const uint32_t m0 = (uint32_t)(n20 + b4) * (uint32_t)k1;
+            float r0 = (float)m0 * invN;
+            if (r0 >= 0.5f) r0 -= 1.0f;
+            float r1 = (float)k1 * invN;
+            if (r1 >= 0.5f) r1 -= 1.0f;
+            const cf w0 = expi_rev(r0), w1 = expi_rev(r1);
+            const cf w2 = cmul(w1, w1);
+            const cf tw[4] = {w0, cmul(w0, w1), cmul(w0, w2), cmul(w0, cmul(w2, w1))};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int64_t m = (n20 + b4 + i) * (int64_t)k1;
-                float rev = (float)m * invN;
-                if (rev >= 0.5f) rev -= 1.0f;
-                if constexpr (!(kAbl & 4)) lds[Lds<N1>::at(b4 + i, k1)] = cmul(a[i], expi_rev(rev)); else lds[Lds<N1>::at(b4 + i, k1)] = a[i];
+                if constexpr (!(kAbl & 4)) lds[Lds<N1>::at(b4 + i, k1)] = cmul(a[i], tw[i]); else lds[Lds<N1>::at(b4 + i, k1)] = a[i];
             }
         }
         __syncthreads();
@@ -1124,15 +1220,24 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
         inv_block(k, k.Yd + (int64_t)pr * k.N, n20, lds, tid);
         const Rng gn(p.seed, p.call_noise, P_NOISE);
+        const uint32_t rbytes = (uint32_t)(k.N * 4);
+        const Buf oa(p.data + (int64_t)max(ra, 0) * p.ld, rbytes), ob(p.data + (int64_t)min(rb, p.nchan - 1) * p.ld, rbytes);
         float acc[ITEMS][2][4];
 #pragma unroll
         for (int t = 0; t < ITEMS; ++t) {
             const int it = tid + t * T;
             const int n1 = it / (B / 4);
             const int b4 = (it - n1 * (B / 4)) * 4;
-            const int64_t n = n1 * N2 + n20 + b4;
-            const float4 xa = chi2_1x4(gn.bits((uint32_t)(n >> 2), ca, (uint32_t)(n >> 34)));
-            const float4 xb = chi2_1x4(gn.bits((uint32_t)(n >> 2), cb, (uint32_t)(n >> 34)));
+            const uint32_t n = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4;   // N <= 2^24
+            float4 xa, xb;
+            if constexpr (kAbl & 1) {
+                const float fn = (float)n;
+                xa = make_float4(fn, fn + 1.f, fn + 2.f, fn + 3.f);
+                xb = make_float4(fn, fn - 1.f, fn - 2.f, fn - 3.f);
+            } else {
+                xa = chi2_1x4(gn.bits(n >> 2, ca, 0u));
+                xb = chi2_1x4(gn.bits(n >> 2, cb, 0u));
+            }
             const float na[4] = {xa.x, xa.y, xa.z, xa.w}, nb[4] = {xb.x, xb.y, xb.z, xb.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -1146,13 +1251,15 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
             const int it = tid + t * T;
             const int n1 = it / (B / 4);
             const int b4 = (it - n1 * (B / 4)) * 4;
-            const int64_t n = n1 * N2 + n20 + b4;
-            if (hasa)
-                *reinterpret_cast<float4 *>(p.data + (int64_t)ra * p.ld + n) =
-                    make_float4(acc[t][0][0], acc[t][0][1], acc[t][0][2], acc[t][0][3]);
-            if (hasb)
-                *reinterpret_cast<float4 *>(p.data + (int64_t)rb * p.ld + n) =
-                    make_float4(acc[t][1][0], acc[t][1][1], acc[t][1][2], acc[t][1][3]);
+            const uint32_t off = ((uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4) * 4u;
+            if constexpr (kAbl & 64) {   // ablation: contiguous stores (wrong place)
+                const uint32_t o2 = ((uint32_t)(cbx * T * ITEMS) + (uint32_t)it) * 16u;
+                if (hasa) oa.st4(acc[t][0][0], acc[t][0][1], acc[t][0][2], acc[t][0][3], o2, 0);
+                if (hasb) ob.st4(acc[t][1][0], acc[t][1][1], acc[t][1][2], acc[t][1][3], o2, 0);
+                continue;
+            }
+            if (hasa) oa.st4(acc[t][0][0], acc[t][0][1], acc[t][0][2], acc[t][0][3], off, 0);
+            if (hasb) ob.st4(acc[t][1][0], acc[t][1][1], acc[t][1][2], acc[t][1][3], off, 0);
         }
     }
 
@@ -1469,7 +1576,7 @@ static inline int64_t al256(int64_t b) { return (b + 255) & ~255ll; }
 static inline bool fourstep_len(int64_t n) { return is_pow2(n) && n >= 16384 && n <= (1ll << 24); }
 
 struct WsLayout {
-    int64_t yd, mspec, ynode, nodes, bits, base, coef, misc, mbits, row, total;
+    int64_t yd, mspec, ynode, nodes, bits, base, coef, misc, mbits, rtab, row, total;
 };
 
 static WsLayout ws_layout(int32_t nchan, int64_t N) {
@@ -1487,6 +1594,7 @@ static WsLayout ws_layout(int32_t nchan, int64_t N) {
         w.coef = o;  o += al256(N * KCH * 4);
         w.misc = o;  o += 256;
         w.mbits = o; o += al256((int64_t)nchan * (N / 8));   // per-channel null bits
+        w.rtab = o;  o += al256((int64_t)nchan * 64 * 8);     // row-pass ramp factors (RFL <= 64)
     } else if (!(is_pow2(N) && N >= 64 && N <= 8192)) {
         o += al256(2 * (int64_t)nchan * N * 8 + N * 8);    // fallback: W1, W2, twiddles
     }
@@ -1502,7 +1610,8 @@ static int g_flags = 0;   // pss_set_flags (test hook)
 
 static bool fast_source(const PssPipeline &p) {
     if (g_flags & PSS_FLAG_NO_FAST) return false;
-    return p.src == PSS_SRC_SEARCH && p.gen_df == 1.0f && !p.inj_gen && p.null_mode != PSS_NULL_UNDELAYED;
+    return p.src == PSS_SRC_SEARCH && p.gen_df == 1.0f && !p.inj_gen && p.null_mode != PSS_NULL_UNDELAYED &&
+           p.nint <= kFastNint;
 }
 static bool fast_epilogue(const KP &k) {
     const PssPipeline &p = k.p;
@@ -1605,6 +1714,12 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
         tk_end(st);
         LAUNCHCHK();
         return PSS_OK;
+    }
+    {
+        cf *rt = reinterpret_cast<cf *>(w + L.rtab);
+        k_ramp_tab<PR::RFL><<<dim3((unsigned)k.p.nchan), dim3(64), 0, st>>>(k.p.ramp, k.N, k.p.nchan, rt);
+        LAUNCHCHK();
+        k.rtab = rt;
     }
     dim3 gc((unsigned)(N2 / B), (unsigned)k.npairs);
     tk_begin(TK_COLA, st);
