@@ -197,6 +197,25 @@ int pss_clip_cast(const float *in, void *out, int64_t count, float clip, int32_t
 int pss_fold(const float *data, float *out, int32_t nchan, int64_t ld, int64_t npbins,
              int64_t n_fold, void *stream);
 
+/*
+ * Native host planning (no GPU; bitwise replicas of the float64 NumPy
+ * arithmetic in psrsigsim_amd/pulsar/portraits.py, itself pinned to the
+ * reference's scipy PCHIP -- pulsar/portraits.py:200-267 of the reference).
+ * `nthreads` host threads split the rows.
+ *   pss_host_pchip_coef:   c[rows][K-1][4] piecewise-cubic coefficients
+ *                          (powers 3..0 of t - x_i) through y[rows][K] at x[K]
+ *   pss_host_ppoly_eval:   out[rows][n] = the cubic at phases ph[n]
+ *                          (interval = last x_i <= phase, end pieces extrapolate)
+ *   pss_host_device_table: out[rows][nint][4] (float32) = c * (h^3, h^2, h, 1)
+ *                          / amax (the table the source stage evaluates)
+ */
+int pss_host_pchip_coef(const double *x, int64_t K, const double *y, int64_t rows, double *c,
+                        int nthreads);
+int pss_host_ppoly_eval(const double *x, int64_t K, const double *c, int64_t rows, const double *ph,
+                        int64_t n, double *out, int nthreads);
+int pss_host_device_table(const double *c, int64_t rows, int64_t nint, double h, double amax,
+                          float *out, int nthreads);
+
 /* Philox chi2 draws (test hook + CPU-independent statistics checks):
  * out[r][n] = chi2(df) keyed like the pipeline's purpose `purpose`. */
 int pss_chi2_fill(float *out, int32_t nrows, int32_t chan0, int64_t n, float df,

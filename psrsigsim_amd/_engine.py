@@ -19,6 +19,7 @@ channel, sample) -- see ``seed()``; exact replay of the reference's own draws
 is available through ``inject()`` (tests).
 """
 import ctypes
+import os
 import threading
 
 import numpy as np
@@ -91,17 +92,33 @@ def stream_ptr():
 _ws = {}
 
 
-def workspace(nbytes):
-    """Cached per-device workspace (grown on demand, never shrunk)."""
+def workspace(nbytes, role="main"):
+    """Cached per-device workspace (grown on demand, never shrunk).  The
+    channel-0 probe has its own (``role="probe"``): it runs on a side stream
+    while the previous main run may still be using the main one."""
     dev = device()
-    buf = _ws.get(dev.index)
+    key = (dev.index, role)
+    buf = _ws.get(key)
     if nbytes <= 0:
         return None
     if buf is None or buf.numel() < nbytes:
-        _ws.pop(dev.index, None)
+        _ws.pop(key, None)
         buf = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
-        _ws[dev.index] = buf
+        _ws[key] = buf
     return buf
+
+
+_probe_streams = {}
+
+
+def probe_stream():
+    """Side stream of the channel-0 probe (per device)."""
+    dev = device()
+    s = _probe_streams.get(dev.index)
+    if s is None:
+        s = torch.cuda.Stream(device=dev, priority=-1)
+        _probe_streams[dev.index] = s
+    return s
 
 
 def release_workspace():
@@ -109,10 +126,14 @@ def release_workspace():
 
 
 def to_dev(a, dtype=None):
+    """Host array -> device tensor, stream-ordered and without blocking the
+    host: from pageable memory the copy would wait for the stream to drain
+    (i.e. for the previous signal's fused run), so it goes through a pinned
+    staging copy (torch's caching host allocator) and a non-blocking copy."""
     t = torch.as_tensor(np.ascontiguousarray(a))
     if dtype is not None:
         t = t.to(dtype)
-    return t.to(device())
+    return t.pin_memory().to(device(), non_blocking=True)
 
 
 def ptr(t):
@@ -232,7 +253,7 @@ def plan_pipeline(sig, pend, rows, chan0):
     return P
 
 
-def build_pipeline(sig, pend, rows, chan0, data, out=None):
+def build_pipeline(sig, pend, rows, chan0, data, out=None, ws_role="main"):
     """A PssPipeline (plus the device buffers it points at) for local rows
     [0, rows) of ``data`` holding global channels [chan0, chan0+rows)."""
     P = plan_pipeline(sig, pend, rows, chan0)
@@ -255,7 +276,7 @@ def build_pipeline(sig, pend, rows, chan0, data, out=None):
         keep.append(t)
         setattr(p, name, ptr(t))
     if P.get("shift"):
-        ws = workspace(_lib.load().pss_workspace_bytes(rows, sig._ncols))
+        ws = workspace(_lib.load().pss_workspace_bytes(rows, sig._ncols), ws_role)
         p.work = ptr(ws) if ws is not None else None
     if out is not None:
         p.out_kind = out["kind"]
@@ -302,8 +323,10 @@ def probe_row0(sig, pend, count):
     channel-0 shadow."""
     N = sig._ncols
     nrow = min(2, sig.Nchan)
-    scratch = torch.empty((nrow, N), dtype=torch.float32, device=device())
+    main = torch.cuda.current_stream()
     if pend.source is None:
+        # replaying from existing device data: ordered after the main stream
+        scratch = torch.empty((nrow, N), dtype=torch.float32, device=device())
         if sig._c0 == 0 and sig._c1 >= nrow:
             base = sig._buf[0:nrow]
         else:
@@ -311,10 +334,36 @@ def probe_row0(sig, pend, count):
         if base is None:
             raise RuntimeError("no data for channel 0")
         scratch.copy_(base)
-    probe = Pending(pend.source)
-    probe.shifts = list(pend.shifts)
-    probe.null = pend.null
-    if not probe.empty():
-        p, keep = build_pipeline(sig, probe, nrow, 0, scratch)
-        run(p, keep)
-    return scratch[0, :count].cpu().numpy().astype(np.float64)
+        side = main
+    else:
+        # regenerated from the source: independent of whatever the main
+        # stream is still running (e.g. the previous signal's fused run), so
+        # it goes to a high-priority side stream with its own workspace.
+        # (Measured on MI355X: its kernels still start only after the main
+        # run's big launches drain -- no interleaving -- so what this buys is
+        # that nothing on the host waits for the device except the probe.)
+        side = probe_stream()
+        if getattr(pend.source, "dev_table", None) is not None:
+            side.wait_stream(main)               # table uploaded on the main stream
+    with torch.cuda.stream(side):
+        if pend.source is not None:
+            scratch = torch.empty((nrow, N), dtype=torch.float32, device=device())
+        probe = Pending(pend.source)
+        probe.shifts = list(pend.shifts)
+        probe.null = pend.null
+        if not probe.empty():
+            p, keep = build_pipeline(sig, probe, nrow, 0, scratch, ws_role="probe")
+            run(p, keep)
+        # pinned, non-blocking read-back + an event on this stream: waits for
+        # the probe only (a pageable .cpu() would wait for the device)
+        row0 = torch.empty(count, dtype=torch.float32, pin_memory=True)
+        row0.copy_(scratch[0, :count], non_blocking=True)
+        done = torch.cuda.Event()
+        done.record(side)
+    done.synchronize()
+    if side is not main:
+        main.wait_stream(side)
+        dt = getattr(pend.source, "dev_table", None)
+        if dt is not None:
+            dt.record_stream(main)
+    return row0.numpy().astype(np.float64)

@@ -59,6 +59,10 @@ EXPORTS = {
     "pss_clip_cast": (ctypes.c_int, [c_vp, c_vp, c_i64, c_f32, c_i32, c_vp]),
     "pss_fold": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp]),
     "pss_chi2_fill": (ctypes.c_int, [c_vp, c_i32, c_i32, c_i64, c_f32, c_u64, c_u32, c_u32, c_vp]),
+    "pss_host_pchip_coef": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, ctypes.c_int]),
+    "pss_host_ppoly_eval": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, ctypes.c_int]),
+    "pss_host_device_table": (ctypes.c_int, [c_vp, c_i64, c_i64, ctypes.c_double, ctypes.c_double,
+                                             c_vp, ctypes.c_int]),
 }
 
 _LIB = None
@@ -119,3 +123,65 @@ def check(rc, what=""):
     if rc == PSS_EUNSUPPORTED:
         raise NotImplementedError(msg)
     raise RuntimeError(msg)
+
+
+# ---------------------------------------------------------------------------
+# native host planning (pss_host_*): float64 tables, bitwise equal to NumPy
+# ---------------------------------------------------------------------------
+def _tune_host_malloc():
+    """Keep glibc from returning the planning tables' memory to the kernel
+    between signals: (Nchan x Nph) float64 tables are 4-16 MB, above glibc's
+    default mmap threshold, so every fresh table paid ~4k page faults (zeroing)
+    -- most of the per-signal host planning time.  Heap-allocate up to 32 MB
+    and trim only above 512 MB of free heap."""
+    try:
+        libc = ctypes.CDLL("libc.so.6")
+        M_TRIM_THRESHOLD, M_MMAP_THRESHOLD = -1, -3
+        libc.mallopt(M_MMAP_THRESHOLD, 32 << 20)
+        libc.mallopt(M_TRIM_THRESHOLD, 512 << 20)
+    except OSError:
+        pass
+
+
+if os.environ.get("PSS_NO_MALLOPT") is None:
+    _tune_host_malloc()
+
+
+def host_threads():
+    n = os.environ.get("PSS_HOST_THREADS")
+    return max(1, int(n)) if n else max(1, min(8, os.cpu_count() or 1))
+
+
+def _dptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def host_pchip_coef(x, y):
+    import numpy as np
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    rows, K = y.shape
+    c = np.empty((rows, K - 1, 4))
+    check(load().pss_host_pchip_coef(_dptr(x), K, _dptr(y), rows, _dptr(c), host_threads()),
+          "pss_host_pchip_coef")
+    return c
+
+
+def host_ppoly_eval(x, c, ph):
+    import numpy as np
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    c = np.ascontiguousarray(c, dtype=np.float64)
+    ph = np.ascontiguousarray(ph, dtype=np.float64).ravel()
+    out = np.empty((c.shape[0], ph.size))
+    check(load().pss_host_ppoly_eval(_dptr(x), x.size, _dptr(c), c.shape[0], _dptr(ph), ph.size,
+                                     _dptr(out), host_threads()), "pss_host_ppoly_eval")
+    return out
+
+
+def host_device_table(c, h, amax):
+    import numpy as np
+    c = np.ascontiguousarray(c, dtype=np.float64)
+    out = np.empty(c.shape, dtype=np.float32)
+    check(load().pss_host_device_table(_dptr(c), c.shape[0], c.shape[1], float(h), float(amax),
+                                       _dptr(out), host_threads()), "pss_host_device_table")
+    return out

@@ -5,7 +5,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = [os.path.join(HERE, "csrc", "pss_pipeline.hip")]
+SRC = [os.path.join(HERE, "csrc", "pss_pipeline.hip"), os.path.join(HERE, "csrc", "pss_host.cpp")]
 DEPS = SRC + [os.path.join(HERE, "csrc", f) for f in ("pss_device.hpp", "pss_fft.hpp")] + \
     [os.path.join(ROOT, "include", "pss_hip.h")]
 OUT = os.path.join(HERE, "libpss_hip.so")

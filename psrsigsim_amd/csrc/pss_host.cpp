@@ -1,0 +1,147 @@
+// pss_host.cpp -- native host planning for the profile-level tables.
+//
+// The profile tables the device path evaluates (PCHIP coefficients of every
+// channel's portrait, their evaluation at resampling phases, the float32
+// device table) are O(Nchan x Nph) float64 work done once per signal on the
+// host.  The NumPy formulation spends its time on (Nchan x Nph) temporaries
+// (page faults, memory traffic); these loops do one pass per row, spread over
+// host threads, with EXACTLY the operations and order of the NumPy code they
+// replace (psrsigsim_amd/pulsar/portraits.py: pchip_coefficients, ppoly_eval,
+// DataPortrait.device_table), so results are bitwise identical -- the reference
+// makes exact float decisions on these values (portraits.py:234).
+//
+// No FMA contraction anywhere in this file (numpy evaluates each binary op
+// separately in IEEE double).
+#pragma clang fp contract(off)
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+#include "../../include/pss_hip.h"
+
+namespace {
+
+// np.sign as a double: -1, 0, +1, NaN for NaN
+inline double sgn(double v) { return v > 0.0 ? 1.0 : (v < 0.0 ? -1.0 : (v == 0.0 ? 0.0 : v)); }
+
+// portraits.py _edge_slope (scipy's one-sided three-point end slope + clamps)
+inline double edge_slope(double h0, double h1, double m0, double m1) {
+    double d = ((2.0 * h0 + h1) * m0 - h0 * m1) / (h0 + h1);
+    const bool flip = sgn(d) != sgn(m0);          // NaN compares unequal, as in numpy
+    const bool big = (sgn(m0) != sgn(m1)) && (fabs(d) > 3.0 * fabs(m0));
+    if (flip) d = 0.0;
+    return (!flip && big) ? 3.0 * m0 : d;
+}
+
+template <typename F>
+void parallel_rows(int64_t rows, int nthreads, F fn) {
+    if (nthreads <= 1 || rows < 64) {
+        fn(0, rows);
+        return;
+    }
+    const int nt = (int)std::min<int64_t>(nthreads, rows / 32);
+    std::vector<std::thread> th;
+    th.reserve(nt);
+    for (int t = 0; t < nt; ++t) {
+        const int64_t a = rows * t / nt, b = rows * (t + 1) / nt;
+        th.emplace_back([=] { fn(a, b); });
+    }
+    for (auto &x : th) x.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+int pss_host_pchip_coef(const double *x, int64_t K, const double *y, int64_t rows, double *c,
+                        int nthreads) {
+    if (K < 2 || rows < 0 || !x || !y || !c) return PSS_EINVAL;
+    std::vector<double> h(K - 1);
+    for (int64_t i = 0; i + 1 < K; ++i) h[i] = x[i + 1] - x[i];
+    parallel_rows(rows, nthreads, [&](int64_t r0, int64_t r1) {
+        std::vector<double> m(K - 1), d(K);
+        for (int64_t r = r0; r < r1; ++r) {
+            const double *yr = y + r * K;
+            for (int64_t i = 0; i + 1 < K; ++i) m[i] = (yr[i + 1] - yr[i]) / h[i];
+            if (K == 2) {
+                d[0] = d[1] = m[0];
+            } else {
+                for (int64_t i = 1; i + 1 < K; ++i) {
+                    const double m0 = m[i - 1], m1 = m[i];
+                    const double w1 = 2.0 * h[i] + h[i - 1];
+                    const double w2 = h[i] + 2.0 * h[i - 1];
+                    const bool flat = (std::signbit(m0) != std::signbit(m1)) || (m1 == 0.0) || (m0 == 0.0);
+                    d[i] = flat ? 0.0 : 1.0 / ((w1 / m0 + w2 / m1) / (w1 + w2));
+                }
+                d[0] = edge_slope(h[0], h[1], m[0], m[1]);
+                d[K - 1] = edge_slope(h[K - 2], h[K - 3], m[K - 2], m[K - 3]);
+            }
+            double *cr = c + r * (K - 1) * 4;
+            for (int64_t i = 0; i + 1 < K; ++i) {
+                const double d0 = d[i], d1 = d[i + 1], hi = h[i], mi = m[i];
+                const double t = (d0 + d1 - 2.0 * mi) / hi;
+                cr[4 * i + 0] = t / hi;
+                cr[4 * i + 1] = (mi - d0) / hi - t;
+                cr[4 * i + 2] = d0;
+                cr[4 * i + 3] = yr[i];
+            }
+        }
+    });
+    return PSS_OK;
+}
+
+int pss_host_ppoly_eval(const double *x, int64_t K, const double *c, int64_t rows, const double *ph,
+                        int64_t n, double *out, int nthreads) {
+    if (K < 2 || rows < 0 || n < 0 || !x || !c || !ph || !out) return PSS_EINVAL;
+    // interval = last breakpoint <= phase (searchsorted 'right' - 1), clipped
+    // to the end pieces; s = phase - x[i]
+    std::vector<int64_t> iv(n);
+    std::vector<double> s(n);
+    for (int64_t j = 0; j < n; ++j) {
+        int64_t i = (int64_t)(std::upper_bound(x, x + K, ph[j]) - x) - 1;
+        i = std::min<int64_t>(std::max<int64_t>(i, 0), K - 2);
+        iv[j] = i;
+        s[j] = ph[j] - x[i];
+    }
+    parallel_rows(rows, nthreads, [&](int64_t r0, int64_t r1) {
+        for (int64_t r = r0; r < r1; ++r) {
+            const double *cr = c + r * (K - 1) * 4;
+            double *o = out + r * n;
+            for (int64_t j = 0; j < n; ++j) {
+                const double *ci = cr + 4 * iv[j];
+                const double sj = s[j];
+                double res = ci[3] * 1.0;
+                double z = sj;
+                res = res + ci[2] * z;
+                z = z * sj;
+                res = res + ci[1] * z;
+                z = z * sj;
+                res = res + ci[0] * z;
+                o[j] = res;
+            }
+        }
+    });
+    return PSS_OK;
+}
+
+int pss_host_device_table(const double *c, int64_t rows, int64_t nint, double h, double amax,
+                          float *out, int nthreads) {
+    if (rows < 0 || nint < 1 || !c || !out) return PSS_EINVAL;
+    const double w[4] = {pow(h, 3.0), pow(h, 2.0), h, 1.0};   // np.array([h ** 3, h ** 2, h, 1.0])
+    const bool div = amax != 1.0;
+    parallel_rows(rows, nthreads, [&](int64_t r0, int64_t r1) {
+        for (int64_t e = r0 * nint * 4; e < r1 * nint * 4; ++e) {
+            double v = c[e] * w[e & 3];
+            if (div) v = v / amax;
+            out[e] = (float)v;
+        }
+    });
+    return PSS_OK;
+}
+
+}  // extern "C"

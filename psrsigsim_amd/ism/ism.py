@@ -7,11 +7,13 @@ delay stages run as ONE forward/inverse FFT pass on the GPU (the reference runs
 one rfft/irfft pair per channel per call: ism.py:57-60, 136-139, 203-206).
 """
 import numpy as np
+from scipy import fft as _sp_fft
 from scipy.signal import fftconvolve as _fftconvolve
 
 from ..utils.constants import DM_K_VALUE, KOLMOGOROV_BETA
 from ..utils.utils import make_quant
 from .._units import Quantity, to_value
+from .. import _lib
 from ..pulsar.portraits import DataPortrait
 from .. import _engine
 
@@ -112,7 +114,8 @@ class ISM(object):
         # scipy's FFT convolution batched over rows: bit-identical to the
         # reference's per-row scipy.signal.convolve(..., method='fft') (the
         # reference later makes exact float decisions on these values).
-        conv = _fftconvolve(pn, kn, mode='full', axes=1)
+        with _sp_fft.set_workers(_lib.host_threads()):    # pocketfft threads over rows
+            conv = _fftconvolve(pn, kn, mode='full', axes=1)
         profiles[:rows, :] = ps * conv[:, :width]
         return profiles
 

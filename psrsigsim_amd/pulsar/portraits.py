@@ -16,10 +16,12 @@ import logging
 
 import numpy as np
 
+from .. import _lib
+
 log = logging.getLogger("psrsigsim_amd")
 
 __all__ = ["PulsePortrait", "GaussPortrait", "DataPortrait", "UserPortrait",
-           "pchip_slopes", "pchip_coefficients", "ppoly_eval"]
+           "pchip_slopes", "pchip_coefficients", "pchip_coefficients_np", "ppoly_eval", "ppoly_eval_np"]
 
 
 # ---------------------------------------------------------------------------
@@ -59,7 +61,14 @@ def pchip_slopes(x, y, h=None, m=None):
 
 
 def pchip_coefficients(x, y):
-    """Piecewise-cubic coefficients [rows, K-1, 4] in powers (t - x_i)^(3..0)."""
+    """Piecewise-cubic coefficients [rows, K-1, 4] in powers (t - x_i)^(3..0).
+    Computed natively (pss_host_pchip_coef, one pass per row, host threads);
+    bitwise equal to :func:`pchip_coefficients_np`."""
+    return _lib.host_pchip_coef(x, np.atleast_2d(np.asarray(y, dtype=float)))
+
+
+def pchip_coefficients_np(x, y):
+    """NumPy statement of :func:`pchip_coefficients` (the tested reference)."""
     x = np.asarray(x, dtype=float)
     y = np.asarray(y, dtype=float)
     h = np.diff(x)
@@ -88,6 +97,12 @@ def ppoly_eval(x, c, ph, y=None):
     ph = np.asarray(ph, dtype=float)
     if y is not None and ph.size <= x.size and np.array_equal(ph, x[:ph.size]):
         return np.array(y[:, :ph.size])
+    return _lib.host_ppoly_eval(x, c, ph)
+
+
+def ppoly_eval_np(x, c, ph):
+    """NumPy statement of :func:`ppoly_eval` (the tested reference)."""
+    ph = np.asarray(ph, dtype=float)
     i = np.clip(np.searchsorted(x, ph, side="right") - 1, 0, x.size - 2)
     s = (ph - x[i])[None, :]
     ci = c[:, i, :]
@@ -280,10 +295,8 @@ class DataPortrait(PulsePortrait):
         M, nint = geo
         h = 1.0 / M
         amax = self.Amax if hasattr(self, '_Amax') else 1.0
-        tab = self._coef * np.array([h ** 3, h ** 2, h, 1.0])     # [rows, nint, 4]
-        if amax != 1.0:
-            tab = tab / amax
-        return np.ascontiguousarray(tab, dtype=np.float32), M, nint
+        # = (self._coef * [h**3, h**2, h, 1] / amax).astype(float32), natively
+        return _lib.host_device_table(self._coef, h, amax), M, nint
 
 
 class UserPortrait(PulsePortrait):

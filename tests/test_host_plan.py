@@ -189,3 +189,61 @@ def test_scatter_convolution_bitwise_vs_reference_structure(nchan):
     opsr.ref_freq = 1400.0
     O.add_spec_idx(osig, opsr)
     assert sig._pending.source.nint == opsr.Profiles.knot_x.size - 1
+
+
+# ---------------------------------------------------------------------------
+# native host planning (pss_host_*) == the NumPy statements, bit for bit
+# ---------------------------------------------------------------------------
+def _pchip_cases():
+    rng = np.random.default_rng(5)
+    x = np.arange(245) / 244.0
+    y = rng.random((300, 245))
+    y[:40, 100:130] = 0.25                 # flat runs (zero slopes)
+    y[40:80] = np.sin(np.linspace(0, 12, 245))[None, :] * rng.random((40, 1))   # sign changes
+    y[80:90] = 0.0                         # all-zero rows
+    y[90:100, ::7] = -y[90:100, ::7]       # alternating monotonicity breaks
+    xs = np.sort(np.concatenate([[0.0, 1.0], rng.random(30)]))   # non-uniform knots
+    return [(x, y), (x[:3], y[:5, :3]), (x[:2], y[:4, :2]), (xs, rng.random((70, xs.size)))]
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_native_pchip_bitwise(case):
+    from psrsigsim_amd import _lib
+    from psrsigsim_amd.pulsar.portraits import pchip_coefficients_np, ppoly_eval_np
+    x, y = _pchip_cases()[case]
+    c_np = pchip_coefficients_np(x, y)
+    c = _lib.host_pchip_coef(x, y)
+    np.testing.assert_array_equal(c, c_np)
+    ph = np.concatenate([np.linspace(-0.1, 1.1, 333), x, [0.5 / 244.0]])
+    np.testing.assert_array_equal(_lib.host_ppoly_eval(x, c_np, ph), ppoly_eval_np(x, c_np, ph))
+
+
+def test_native_device_table_bitwise():
+    from psrsigsim_amd import _lib
+    from psrsigsim_amd.pulsar.portraits import pchip_coefficients_np
+    x, y = _pchip_cases()[0]
+    c = pchip_coefficients_np(x, y)
+    h = 1.0 / 244
+    for amax in (1.0, 0.7316):
+        ref = c * np.array([h ** 3, h ** 2, h, 1.0])
+        if amax != 1.0:
+            ref = ref / amax
+        np.testing.assert_array_equal(_lib.host_device_table(c, h, amax), ref.astype(np.float32))
+
+
+def test_native_threads_invariant():
+    import os
+    from psrsigsim_amd import _lib
+    x, y = _pchip_cases()[0]
+    old = os.environ.get("PSS_HOST_THREADS")
+    try:
+        os.environ["PSS_HOST_THREADS"] = "1"
+        a = _lib.host_pchip_coef(x, y)
+        os.environ["PSS_HOST_THREADS"] = "7"
+        b = _lib.host_pchip_coef(x, y)
+    finally:
+        if old is None:
+            os.environ.pop("PSS_HOST_THREADS", None)
+        else:
+            os.environ["PSS_HOST_THREADS"] = old
+    np.testing.assert_array_equal(a, b)
