@@ -34,6 +34,11 @@ static constexpr int kAbl = PSS_ABLATE;
 #endif
 static constexpr bool kXcdMap = PSS_XCD_MAP != 0;
 static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
+// fast pass C block width / threads for N = 2^22 (1024 x 4096 split)
+#ifndef PSS_BC
+#define PSS_BC 16
+#define PSS_TC 1024
+#endif
 
 
 using namespace pss;
@@ -1692,10 +1697,14 @@ static int build_mask_table(KP &k, hipStream_t st, const float *mask_row, char *
     return PSS_OK;
 }
 
+// BC/TC: column-block width and threads of the FAST pass C (the spill layout
+// does not depend on the block width, so pass C may use wider blocks than pass
+// A: its output rows are written in BC-sample (4 BC-byte) segments).
 template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typename RF, typename RI,
-          int TRF>
+          int TRF, int BC = B, int TC = T>
 static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
     using PC = PairCols<N1, B, T, CF, CI>;
+    using PCC = PairCols<N1, BC, TC, CF, CI>;
     using PR = PairRows<N2, TR, RF, RI>;
     k.poff = k.p.chan0 & 1;
     k.npairs = (k.p.nchan + k.poff + 1) / 2;
@@ -1733,7 +1742,7 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
     LAUNCHCHK();
     const bool fast = fast_epilogue(k);
     tk_begin(TK_COLC, st);
-    if (fast) k_pairC_fast<PC, T><<<gc, dim3(T), 0, st>>>(k);
+    if (fast) k_pairC_fast<PCC, TC><<<dim3((unsigned)(N2 / BC), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
     else k_pairC<PC, T><<<gc, dim3(T), 0, st>>>(k);
     tk_end(st);
     LAUNCHCHK();
@@ -1751,7 +1760,7 @@ static int run_fourstep(KP &k, hipStream_t st, const float *mask_row) {
     if (kSplit4k && N == (1 << 22)) {
         k.N2 = 4096;
         k.N1 = 1024;
-        return launch_pair<1024, 8, 512, C1kF, C1kF, 4096, 512, C4k, C4k, 256>(k, st, mask_row);
+        return launch_pair<1024, 8, 512, C1kF, C1kF, 4096, 512, C4k, C4k, 256, PSS_BC, PSS_TC>(k, st, mask_row);
     }
     if (N >= (1 << 17)) {
         k.N2 = 8192;

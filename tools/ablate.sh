@@ -18,7 +18,7 @@ flags_of() {
 if [ "$1" = build ]; then
   for v in $VARIANTS; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fno-slp-vectorize $(flags_of "$v") \
-      -I$R/include -o $R/psrsigsim_amd/libpss_hip_abl$(tag_of "$v").so $R/psrsigsim_amd/csrc/pss_pipeline.hip 2>/dev/null &
+      -I$R/include -o $R/psrsigsim_amd/libpss_hip_abl$(tag_of "$v").so $R/psrsigsim_amd/csrc/pss_pipeline.hip $R/psrsigsim_amd/csrc/pss_host.cpp 2>/dev/null &
   done
   wait
   ls -la $R/psrsigsim_amd/libpss_hip_abl*.so
