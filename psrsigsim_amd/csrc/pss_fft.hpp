@@ -55,11 +55,56 @@ __device__ __forceinline__ cf rot(int k, cf x) {
     return cmul(x, w);
 }
 
-// In-register DFT of a power-of-two size R (recursive radix-2 DIT; with full
-// unrolling every index and twiddle is a compile-time constant).
+template <int R, bool INV>
+__device__ __forceinline__ void dft(cf *a);
+
+// -+i * x (forward multiplies by -i)
+template <bool INV>
+__device__ __forceinline__ cf mul_mi(cf x) { return INV ? make_float2(-x.y, x.x) : make_float2(x.y, -x.x); }
+
+// Radix 3: y1,2 = a0 - (a1 + a2)/2 -+ i sin(2 pi/3) (a1 - a2)  (forward: -)
+template <bool INV>
+__device__ __forceinline__ void dft3(cf *a) {
+    constexpr float S3 = 0.86602540378443865f;
+    const cf t1 = cadd(a[1], a[2]);
+    const cf d = csub(a[1], a[2]);
+    const cf t2 = make_float2(fmaf(-0.5f, t1.x, a[0].x), fmaf(-0.5f, t1.y, a[0].y));
+    const cf r = mul_mi<INV>(make_float2(S3 * d.x, S3 * d.y));
+    a[0] = cadd(a[0], t1);
+    a[1] = cadd(t2, r);
+    a[2] = csub(t2, r);
+}
+
+// Radix 5 (conjugate-pair form): with b1 = a1 + a4, b2 = a2 + a3, d1 = a1 - a4,
+// d2 = a2 - a3:  y1,4 = a0 + c1 b1 + c2 b2 -+ i (s1 d1 + s2 d2),
+//                y2,3 = a0 + c2 b1 + c1 b2 -+ i (s2 d1 - s1 d2)   (forward: -)
+template <bool INV>
+__device__ __forceinline__ void dft5(cf *a) {
+    constexpr float C1 = 0.30901699437494742f, C2 = -0.80901699437494742f;
+    constexpr float S1 = 0.95105651629515357f, S2 = 0.58778525229247313f;
+    const cf b1 = cadd(a[1], a[4]), b2 = cadd(a[2], a[3]);
+    const cf d1 = csub(a[1], a[4]), d2 = csub(a[2], a[3]);
+    const cf r1 = make_float2(fmaf(C2, b2.x, fmaf(C1, b1.x, a[0].x)), fmaf(C2, b2.y, fmaf(C1, b1.y, a[0].y)));
+    const cf r2 = make_float2(fmaf(C1, b2.x, fmaf(C2, b1.x, a[0].x)), fmaf(C1, b2.y, fmaf(C2, b1.y, a[0].y)));
+    const cf i1 = mul_mi<INV>(make_float2(fmaf(S2, d2.x, S1 * d1.x), fmaf(S2, d2.y, S1 * d1.y)));
+    const cf i2 = mul_mi<INV>(make_float2(fmaf(-S1, d2.x, S2 * d1.x), fmaf(-S1, d2.y, S2 * d1.y)));
+    a[0] = cadd(a[0], cadd(b1, b2));
+    a[1] = cadd(r1, i1);
+    a[4] = csub(r1, i1);
+    a[2] = cadd(r2, i2);
+    a[3] = csub(r2, i2);
+}
+
+// In-register DFT of size R: 3 and 5 directly; powers of two by recursive
+// radix-2 DIT (with full unrolling every index and twiddle is a compile-time
+// constant).
 template <int R, bool INV>
 __device__ __forceinline__ void dft(cf *a) {
-    if constexpr (R == 2) {
+    if constexpr (R == 3) {
+        dft3<INV>(a);
+    } else if constexpr (R == 5) {
+        dft5<INV>(a);
+    } else if constexpr (R == 2) {
         cf t = a[1];
         a[1] = csub(a[0], t);
         a[0] = cadd(a[0], t);

@@ -999,7 +999,10 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
     static constexpr int RI0 = FF::template first<I...>();
     static constexpr int RIL = FF::template last_of<I...>();
     static constexpr int ITEMS = N1 * B / 4 / T;
-    static_assert(ITEMS * 4 * T == N1 * B, "items per thread");
+    // the unrolled fast kernels need a whole number of 4-sample items per
+    // thread (N1 = 2^m); the generic ones loop (any N1, e.g. 30 = 2 * 3 * 5)
+    static constexpr bool kItemsExact = ITEMS * 4 * T == N1 * B;
+    static_assert(B % 4 == 0, "4-sample items");
 
     // A: generate channels a, b into z = d_a + i d_b; column FFTs; twiddle; spill.
     // FAST (host-selected): search-mode source with Philox chi2(1) draws, no
@@ -1018,6 +1021,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
         const int pra = (p.prof_rows == 1) ? 0 : (int)ca, prb = (p.prof_rows == 1) ? 0 : (int)cb;
         const Rng g(p.seed, p.call_gen, P_PULSE);
+        static_assert(!FAST || kItemsExact, "fast pass A: whole items per thread");
         if constexpr (FAST && !(kAbl & 1)) {
             // The pair's two PCHIP rows are staged in LDS (host guarantees
             // nint <= kFastNint), the items are unrolled and branch-free, so
@@ -1184,8 +1188,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         const float invN = k.invN;
         inv_block(k, k.Yd + (int64_t)pr * k.N, n20, lds, tid);
 #pragma unroll 1
-        for (int t = 0; t < ITEMS; ++t) {
-            const int it = tid + t * T;
+        for (int it = tid; it < N1 * B / 4; it += T) {
             const int n1 = it / (B / 4);
             const int b4 = (it - n1 * (B / 4)) * 4;
             const int64_t n = n1 * k.N2 + n20 + b4;
@@ -1212,6 +1215,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
     // of a delayed null are rewritten afterwards by k_null_fix (~10% of the
     // samples; scattered 8192 apart in this kernel's column order).
     __device__ static void passC_fast(const KP &k) {
+        static_assert(kItemsExact, "fast pass C: whole items per thread");
         __shared__ __align__(16) cf lds[B * Lds<N1>::RS];
         const int tid = threadIdx.x;
         int cbx, pr;
@@ -1580,6 +1584,28 @@ using C8kI = RList<8, 8, 8, 16>;
 static inline int64_t al256(int64_t b) { return (b + 255) & ~255ll; }
 static inline bool fourstep_len(int64_t n) { return is_pow2(n) && n >= 16384 && n <= (1ll << 24); }
 
+// Mixed-radix four-step lengths: even N = N1 * N2 with N2 = 2^m in
+// [1024, 8192] (the largest such power that leaves N1 even) and N1 one of the
+// {2, 3, 4, 5}-smooth column lengths below (e.g. the fold-mode C4 length
+// 30720 = 30 x 1024).  Other even lengths take the direct path.
+static inline bool smooth_col(int64_t n1) {
+    switch (n1) {
+        case 6: case 10: case 12: case 20: case 24: case 30: case 40: case 48: case 60: return true;
+        default: return false;
+    }
+}
+static inline bool smooth_split(int64_t n, int64_t *N1 = nullptr, int64_t *N2 = nullptr) {
+    if (n <= 0 || (n & 1) || is_pow2(n) || n > (1ll << 24)) return false;
+    int v2 = __builtin_ctzll((unsigned long long)n);
+    const int m = v2 - 1 < 13 ? v2 - 1 : 13;            // keep N1 even
+    if (m < 10) return false;
+    const int64_t n2 = 1ll << m, n1 = n / n2;
+    if (!smooth_col(n1)) return false;
+    if (N1) *N1 = n1;
+    if (N2) *N2 = n2;
+    return true;
+}
+
 struct WsLayout {
     int64_t yd, mspec, ynode, nodes, bits, base, coef, misc, mbits, rtab, row, total;
 };
@@ -1602,6 +1628,13 @@ static WsLayout ws_layout(int32_t nchan, int64_t N) {
         w.rtab = o;  o += al256((int64_t)nchan * 64 * 8);     // row-pass ramp factors (RFL <= 64)
     } else if (!(is_pow2(N) && N >= 64 && N <= 8192)) {
         o += al256(2 * (int64_t)nchan * N * 8 + N * 8);    // fallback: W1, W2, twiddles
+        if (smooth_split(N)) {
+            // mixed-radix four-step (inside the same bytes: the direct path
+            // still serves these lengths for a delayed null)
+            const int64_t npairs = ((int64_t)nchan + 2) / 2;
+            w.yd = 0;
+            w.rtab = al256(npairs * N * 8);
+        }
     }
     w.row = o;
     o += al256(N * 4);
@@ -1712,8 +1745,14 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
     const WsLayout L = ws_layout(k.p.nchan, k.N);
     k.Yd = reinterpret_cast<cf *>(w + L.yd);
     if (k.p.null_mode == PSS_NULL_DELAYED) {
-        const int rc = build_mask_table<N1, B, T, CF, CI, N2, TR, RF, RI, TRF>(k, st, mask_row, w, L);
-        if (rc) return rc;
+        // the mask table's position arithmetic is for N = 2^m (validate()
+        // sends delayed nulls of other lengths to the direct path)
+        if constexpr ((N1 & (N1 - 1)) == 0) {
+            const int rc = build_mask_table<N1, B, T, CF, CI, N2, TR, RF, RI, TRF>(k, st, mask_row, w, L);
+            if (rc) return rc;
+        } else {
+            return fail(PSS_EUNSUPPORTED, "delayed null on the mixed-radix four-step (N=%lld)", (long long)k.N);
+        }
     }
     if (!k.p.data_in_fft) {
         // only the null mask was delayed: one elementwise pass with table lookups
@@ -1732,18 +1771,26 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
     }
     dim3 gc((unsigned)(N2 / B), (unsigned)k.npairs);
     tk_begin(TK_COLA, st);
-    if (fast_source(k.p)) k_pairA_fast<PC, T><<<gc, dim3(T), 0, st>>>(k);
-    else k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
+    if constexpr (PC::kItemsExact) {
+        if (fast_source(k.p)) k_pairA_fast<PC, T><<<gc, dim3(T), 0, st>>>(k);
+        else k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
+    } else {
+        k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
+    }
     tk_end(st);
     LAUNCHCHK();
     tk_begin(TK_ROW, st);
     k_pair_row<PR, TR><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
     tk_end(st);
     LAUNCHCHK();
-    const bool fast = fast_epilogue(k);
+    const bool fast = PCC::kItemsExact && fast_epilogue(k);
     tk_begin(TK_COLC, st);
-    if (fast) k_pairC_fast<PCC, TC><<<dim3((unsigned)(N2 / BC), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
-    else k_pairC<PC, T><<<gc, dim3(T), 0, st>>>(k);
+    if (fast) {
+        if constexpr (PCC::kItemsExact)
+            k_pairC_fast<PCC, TC><<<dim3((unsigned)(N2 / BC), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
+    } else {
+        k_pairC<PC, T><<<gc, dim3(T), 0, st>>>(k);
+    }
     tk_end(st);
     LAUNCHCHK();
     if (fast && k.mtab) {
@@ -1795,6 +1842,39 @@ static int run_fourstep(KP &k, hipStream_t st, const float *mask_row) {
         default: break;
     }
     return fail(PSS_EUNSUPPORTED, "four-step: N=%lld", (long long)N);
+}
+
+// Mixed-radix four-step (see smooth_split): columns of N1 in registers (one
+// column per thread, B = T columns per workgroup), rows by the power-of-two
+// row engine.  Generic (looped) column kernels; no mask table.
+template <int N1, typename CF, typename CI, int T>
+static int launch_smooth_n2(KP &k, hipStream_t st) {
+    switch (k.N2) {
+        case 1024: return launch_pair<N1, T, T, CF, CI, 1024, 128, C1kF, C1kI, 64>(k, st, nullptr);
+        case 2048: return launch_pair<N1, T, T, CF, CI, 2048, 256, C2kF, C2kI, 128>(k, st, nullptr);
+        case 4096: return launch_pair<N1, T, T, CF, CI, 4096, 512, C4k, C4k, 256>(k, st, nullptr);
+        case 8192: return launch_pair<N1, T, T, CF, CI, 8192, 1024, C8kF, C8kI, 512>(k, st, nullptr);
+        default: return fail(PSS_EUNSUPPORTED, "mixed-radix four-step: N2=%lld", (long long)k.N2);
+    }
+}
+
+static int run_smooth(KP &k, hipStream_t st) {
+    int64_t n1 = 0, n2 = 0;
+    if (!smooth_split(k.N, &n1, &n2)) return fail(PSS_EUNSUPPORTED, "N=%lld", (long long)k.N);
+    k.N1 = n1;
+    k.N2 = n2;
+    switch (n1) {
+        case 6:  return launch_smooth_n2<6, RList<2, 3>, RList<3, 2>, 256>(k, st);
+        case 10: return launch_smooth_n2<10, RList<2, 5>, RList<5, 2>, 256>(k, st);
+        case 12: return launch_smooth_n2<12, RList<4, 3>, RList<3, 4>, 256>(k, st);
+        case 20: return launch_smooth_n2<20, RList<4, 5>, RList<5, 4>, 256>(k, st);
+        case 24: return launch_smooth_n2<24, RList<2, 4, 3>, RList<3, 4, 2>, 256>(k, st);
+        case 30: return launch_smooth_n2<30, RList<2, 3, 5>, RList<5, 3, 2>, 256>(k, st);
+        case 40: return launch_smooth_n2<40, RList<2, 4, 5>, RList<5, 4, 2>, 128>(k, st);
+        case 48: return launch_smooth_n2<48, RList<4, 4, 3>, RList<3, 4, 4>, 128>(k, st);
+        case 60: return launch_smooth_n2<60, RList<4, 3, 5>, RList<5, 3, 4>, 128>(k, st);
+        default: return fail(PSS_EUNSUPPORTED, "N1=%lld", (long long)n1);
+    }
 }
 
 static int run_single(KP &k, hipStream_t st) {
@@ -1938,6 +2018,7 @@ int pss_run(const PssPipeline *p, void *stream) {
     }
     if (is_pow2(N) && N >= 64 && N <= 8192) return run_single(k, st);
     if (is_pow2(N) && N >= 16384 && N <= (1ll << 24)) return run_fourstep(k, st, row);
+    if (smooth_split(N) && p->null_mode != PSS_NULL_DELAYED) return run_smooth(k, st);
     return run_fallback(k, st);
 }
 

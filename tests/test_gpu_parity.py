@@ -22,7 +22,9 @@ def test_golden_replay(name, fused, hip_lib):
 
 
 SIZES = [64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536, 1 << 17, 1 << 18,
-         1 << 20, 244, 1000, 30720]
+         1 << 20, 244, 1000, 30720,
+         # mixed-radix four-step: N1 x N2 = 6 x 2048, 10 x 4096, 30 x 2048, 30 x 4096, 24 x 8192
+         12288, 40960, 61440, 122880, 196608]
 
 
 @pytest.mark.parametrize("N", SIZES)
@@ -93,5 +95,29 @@ def test_fourstep_pair_path_vs_oracle(log2n, nchan, null, fused, hip_lib):
     the delayed-null mask, fused and staged = mask-only FFT) against the
     oracle run with legacy RandomState draws, injected into the GPU run."""
     errs = replay.run_case(None, fused=fused, case=_big_case(log2n, nchan, null=null), seed=log2n)
+    bad = {k: v for k, v in errs.items() if not v <= TOL}
+    assert not bad, errs
+
+
+F0_B1855 = 186.4940812499314404
+
+
+def _c4_case(nchan, null):
+    """BASELINE config C4 (fold mode: 30 subints x 1024 bins = 30720 samples
+    per channel, DM 13.3, radiometer noise) at a few channels: the
+    mixed-radix four-step (30 x 1024) -- or, with a delayed null, the direct
+    path -- against the oracle."""
+    ops = [("make_pulses", 1800.0, "pulses"), ("disperse", 13.299393, "disperse")]
+    if null:
+        ops.append(("null", 0.1, "null"))
+    ops.append(("observe", "Arecibo", "Lband_PUPPI", True, "noise"))
+    return dict(sig=dict(fcent=1400, bw=400, nchan=nchan, samprate=F0_B1855 * 1024 * 1e-6, sublen=60.0,
+                         fold=True),
+                psr=dict(period=1.0 / F0_B1855, Smean=0.005, prof=("gauss", 0.5, 0.05, 1)), ops=ops)
+
+
+@pytest.mark.parametrize("nchan,null", [(3, False), (4, False), (2, True)])
+def test_c4_fold_mixed_radix_vs_oracle(nchan, null, hip_lib):
+    errs = replay.run_case(None, fused=True, case=_c4_case(nchan, null), seed=nchan)
     bad = {k: v for k, v in errs.items() if not v <= TOL}
     assert not bad, errs

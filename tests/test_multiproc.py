@@ -86,3 +86,49 @@ def test_shard_validation():
     from psrsigsim_amd.signal import FilterBankSignal
     with pytest.raises(ValueError):
         FilterBankSignal(1400, 400, Nsubband=8, shard=(4, 12))
+
+
+def test_channel_block_tiles():
+    from psrsigsim_amd.shard import channel_block
+    for nchan in (1, 7, 16, 2048, 2049):
+        for world in (1, 2, 3, 8):
+            blocks = [channel_block(nchan, r, world) for r in range(world)]
+            assert blocks[0][0] == 0 and blocks[-1][1] == nchan
+            assert all(blocks[i][1] == blocks[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in blocks]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        channel_block(8, 2, 2)
+
+
+def _gather_worker(rank, world, port, nchan, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from psrsigsim_amd.shard import channel_block, gather_channels
+    c0, c1 = channel_block(nchan, rank, world)
+    # a folded product: [channels, bins] (+ a trailing axis to check shapes)
+    full = torch.arange(nchan * 12, dtype=torch.float32).reshape(nchan, 6, 2) * 0.5 - 3.0
+    got = gather_channels(full[c0:c1].clone(), nchan, dst=world - 1)
+    ok = (got is None) if rank != world - 1 else bool(torch.equal(got, full))
+    flag = torch.tensor([1 if ok else 0])
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        q.put(int(flag.item()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,nchan", [(2, 16), (3, 10)])
+def test_gather_channels_gloo(world, nchan):
+    """The folded/down-sampled product's gather (RCCL on the GPU path) on
+    gloo: uneven channel blocks, non-zero destination rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, nchan, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) == 1
