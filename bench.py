@@ -65,6 +65,56 @@ def c3_step(pss, nchan_total, shard, nsamp_log2, ret_out=False):
     return sig
 
 
+F0_B1855 = 186.4940812499314404
+
+
+def c4_step(pss, nchan_total, shard, gather):
+    """BASELINE config C4: fold mode, 30 subints x 1024 bins over 30 min
+    (30720 samples per channel: the mixed-radix 30 x 1024 four-step), DM 13.3,
+    Arecibo radiometer noise; the folded filterbank is gathered to rank 0 over
+    RCCL (psrsigsim_amd.shard) inside the step.  Gaussian portrait (the
+    B1855+09 template file is not read at run time)."""
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+    from psrsigsim_amd.ism import ISM
+    from psrsigsim_amd.telescope import telescope as T
+    sig = FilterBankSignal(1400, 400, Nsubband=nchan_total, sample_rate=F0_B1855 * 1024 * 1e-6, sublen=60.0,
+                           fold=True, shard=shard)
+    psr = Pulsar(1.0 / F0_B1855, 0.005, profiles=GaussProfile(0.5, 0.05, 1))
+    psr.make_pulses(sig, tobs=1800.0)
+    ISM().disperse(sig, 13.299393)
+    T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True)
+    if gather:
+        from psrsigsim_amd.shard import gather_channels
+        gather_channels(sig.data, nchan_total)
+    return sig
+
+
+def c5_step(pss, nchan_total, shard, nsamp_log2):
+    """BASELINE config C5 per GPU: search mode, 2^24 samples, DM 500 (delays
+    up to ~7x10^4 samples), Arecibo radiometer noise."""
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+    from psrsigsim_amd.ism import ISM
+    from psrsigsim_amd.telescope import telescope as T
+    sig = FilterBankSignal(1400, 400, Nsubband=nchan_total, fold=False, shard=shard)
+    psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
+    psr.make_pulses(sig, tobs=(1 << nsamp_log2) * TOBS_PER_SAMPLE)
+    ISM().disperse(sig, 500)
+    T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True)
+    return sig
+
+
+WORKLOADS = {
+    "c3": "C3 north-star: FilterBankSignal 2048 ch x 2^22 samp per GPU, GaussProfile P=5 ms, "
+          "scatter_broaden(1e-4 s, convolve) + disperse(DM=100) + null(0.1) + Arecibo Lband_PUPPI radiometer noise",
+    "c4": "C4: fold mode 2048 ch x (30 subints x 1024 bins) per GPU, P=1/186.49 Hz, disperse(DM=13.3) + "
+          "Arecibo noise, RCCL gather of the folded filterbank to rank 0",
+    "c5": "C5 per GPU: 1024 ch x 2^24 samp (8192 ch over 8 GPUs), GaussProfile P=5 ms, disperse(DM=500) + "
+          "Arecibo noise",
+}
+
+
 def cpu_baseline(nch, nsamp_log2):
     """The oracle (NumPy restatement with the reference's call structure:
     per-channel rfft/irfft, legacy RandomState chi2, scipy PCHIP), single
@@ -105,7 +155,17 @@ def main():
     ap.add_argument("--cpu-chans", type=int, default=8, help="oracle sample size (channels)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verbose", action="store_true", help="per-step wall times on stderr")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
+                    help="BASELINE config (default: the north-star C3; c4/c5 are extra measurements)")
     args = ap.parse_args()
+    if args.workload == "c5":
+        if args.nchan == NCHAN:
+            args.nchan = 1024
+        if args.log2n == LOG2N:
+            args.log2n = 24
+    if args.workload == "c4":
+        args.log2n = None
+        args.no_cpu = True
 
     import torch
     import torch.distributed as dist
@@ -129,8 +189,17 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    nsamp = 30720 if args.workload == "c4" else (1 << args.log2n)
+
+    def step():
+        if args.workload == "c4":
+            return c4_step(pss, total, shard, gather=world > 1)
+        if args.workload == "c5":
+            return c5_step(pss, total, shard, args.log2n)
+        return c3_step(pss, total, shard, args.log2n)
+
     for _ in range(args.warmup):
-        s = c3_step(pss, total, shard, args.log2n)
+        s = step()
         del s
     barrier()
     _lib.load().pss_timing_enable(1)
@@ -138,7 +207,9 @@ def main():
     t0 = time.perf_counter()
     marks = []
     for _ in range(args.steps):
-        s = c3_step(pss, total, shard, args.log2n)
+        s = step()
+        if args.workload == "c4":
+            _ = s.data          # fold-mode output is small: materialise it (the gather did when N > 1)
         del s
         marks.append(time.perf_counter())
     torch.cuda.synchronize()
@@ -158,11 +229,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     per_step = elapsed / args.steps
-    units = float(total) * (1 << args.log2n)
+    units = float(total) * nsamp
     value = units / per_step
 
     # dominant kernel of the full-size launches
-    full = C * (1 << args.log2n)
+    full = C * nsamp
     agg = {}
     for kind, ms, u in launches:
         if u != full:
@@ -200,10 +271,8 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(per_step * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (Philox chi2 pulses/noise)",
-            "config": {"workload": "C3 north-star: FilterBankSignal 2048 ch x 2^22 samp per GPU, GaussProfile "
-                                   "P=5 ms, scatter_broaden(1e-4 s, convolve) + disperse(DM=100) + "
-                                   "null(0.1) + Arecibo Lband_PUPPI radiometer noise",
-                       "nchan_per_gpu": C, "nsamp": 1 << args.log2n, "parallelism": "channel-shard x%d" % world},
+            "config": {"workload": WORKLOADS[args.workload],
+                       "nchan_per_gpu": C, "nsamp": nsamp, "parallelism": "channel-shard x%d" % world},
             "gpu_kernel_ms_per_step": round(gpu_ms, 3),
             "kernels": kernels,
             "roofline": roof,

@@ -1809,6 +1809,13 @@ static int run_fourstep(KP &k, hipStream_t st, const float *mask_row) {
         k.N1 = 1024;
         return launch_pair<1024, 8, 512, C1kF, C1kF, 4096, 512, C4k, C4k, 256, PSS_BC, PSS_TC>(k, st, mask_row);
     }
+    if (N == (1 << 24)) {
+        // C5 rows: 2048 x 8192; the fast pass C takes 8 columns per workgroup
+        // (1024 threads, 139 KB LDS) for 32-B output segments instead of 16
+        k.N2 = 8192;
+        k.N1 = 2048;
+        return launch_pair<2048, 4, 512, C2kF, C2kF, 8192, 1024, C8kF, C8kI, 512, 8, 1024>(k, st, mask_row);
+    }
     if (N >= (1 << 17)) {
         k.N2 = 8192;
         k.N1 = N / 8192;

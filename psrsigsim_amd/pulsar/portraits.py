@@ -265,9 +265,21 @@ class DataPortrait(PulsePortrait):
                 profiles[:, -1] = profiles[:, 0]
         self._knots = np.asarray(phases, dtype=float)
         self._kvals = np.asarray(profiles, dtype=float)
-        self._coef = pchip_coefficients(self._knots, self._kvals)
+        self._coef_cache = None
+
+    @property
+    def _coef(self):
+        # built on first use: a fold-mode signal only ever evaluates the
+        # portrait AT its knots (the reference's linspace resampling hits them
+        # exactly), which needs no coefficients
+        if self._coef_cache is None:
+            self._coef_cache = pchip_coefficients(self._knots, self._kvals)
+        return self._coef_cache
 
     def _generator(self, phases):
+        ph = np.asarray(phases, dtype=float)
+        if ph.size <= self._knots.size and np.array_equal(ph, self._knots[:ph.size]):
+            return np.array(self._kvals[:, :ph.size])
         return ppoly_eval(self._knots, self._coef, phases, self._kvals)
 
     def calc_profiles(self, phases, Nchan=None):
