@@ -23,6 +23,7 @@ the roofline of the dominant kernel (HIP events on the launch stream, inside
 the timed region), and the CPU oracle timed on a bounded channel sample.
 """
 import argparse
+import contextlib
 import json
 import os
 import platform
@@ -192,6 +193,12 @@ def main():
     nsamp = 30720 if args.workload == "c4" else (1 << args.log2n)
 
     def step():
+        # the API prints the reference's user warnings (e.g. C4's "sample
+        # rate < Nyquist"); stdout carries only the JSON line
+        with contextlib.redirect_stdout(sys.stderr):
+            return _step()
+
+    def _step():
         if args.workload == "c4":
             return c4_step(pss, total, shard, gather=world > 1)
         if args.workload == "c5":
