@@ -264,6 +264,14 @@ def main():
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
                 "avg_launch_ms": round(avg_ms, 4), "alg_bytes_per_launch": bytes_launch}
+        # measured HBM bytes per launch of this kernel (rocprofv3 PMC passes,
+        # tools/pmc_round.sh + tools/pmc_traffic.py; C3 size only)
+        tj = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+        if args.workload == "c3" and C == NCHAN and nsamp == (1 << LOG2N) and os.path.exists(tj):
+            t = json.load(open(tj)).get(dom)
+            if t:
+                roof["traffic"] = round(t["traffic_bytes"] / 1e9, 3)
+                roof["traffic_unit"] = "GB per launch (PMC, profiles/r01/pmc_traffic.json)"
 
     cpu = None
     if rank == 0 and not args.no_cpu:
