@@ -197,6 +197,13 @@ int pss_clip_cast(const float *in, void *out, int64_t count, float clip, int32_t
 int pss_fold(const float *data, float *out, int32_t nchan, int64_t ld, int64_t npbins,
              int64_t n_fold, void *stream);
 
+/* Corrected fold (extension, no reference
+ * counterpart -- backend.py:34-49 is only valid for exactly four periods):
+ * out[c][b] = sum_{p<nper} data[c][p*nbin + b] over whole periods of `nbin`
+ * samples, float64 accumulation, float32 out. */
+int pss_fold_periods(const float *data, float *out, int32_t nchan, int64_t ld, int64_t nbin,
+                     int64_t nper, void *stream);
+
 /*
  * Native host planning (no GPU; bitwise replicas of the float64 NumPy
  * arithmetic in psrsigsim_amd/pulsar/portraits.py, itself pinned to the

@@ -58,6 +58,7 @@ EXPORTS = {
     "pss_rebin": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp]),
     "pss_clip_cast": (ctypes.c_int, [c_vp, c_vp, c_i64, c_f32, c_i32, c_vp]),
     "pss_fold": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp]),
+    "pss_fold_periods": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp]),
     "pss_chi2_fill": (ctypes.c_int, [c_vp, c_i32, c_i32, c_i64, c_f32, c_u64, c_u32, c_u32, c_vp]),
     "pss_host_pchip_coef": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, ctypes.c_int]),
     "pss_host_ppoly_eval": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, ctypes.c_int]),

@@ -1511,6 +1511,25 @@ __global__ void k_fold(const float *data, float *out, int64_t ld, int64_t npbins
     }
 }
 
+// Whole-period fold: out[c][b] = sum_{p < nper} data[c][p nbin + b], float64
+// accumulation in 8 independent partial sums (8 loads in flight per lane;
+// adjacent lanes read adjacent bins).
+__global__ void k_fold_periods(const float *data, float *out, int64_t ld, int64_t nbin, int64_t nper) {
+    const int c = blockIdx.y;
+    const float *row = data + (int64_t)c * ld;
+    for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nbin;
+         b += (int64_t)gridDim.x * blockDim.x) {
+        double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int64_t p = 0;
+        for (; p + 8 <= nper; p += 8) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s[u] += row[(p + u) * nbin + b];
+        }
+        for (; p < nper; ++p) s[0] += row[p * nbin + b];
+        out[(int64_t)c * nbin + b] = (float)(((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7])));
+    }
+}
+
 __global__ void k_chi2_fill(float *out, int64_t n, int32_t chan0, float df, uint64_t seed,
                             uint32_t call_id, uint32_t purpose) {
     const int r = blockIdx.y;
@@ -2081,6 +2100,17 @@ int pss_fold(const float *data, float *out, int32_t nchan, int64_t ld, int64_t n
     if (nchan <= 0 || npbins < 2) return fail(PSS_EINVAL, "fold geometry");
     dim3 g = stream_grid(npbins / 2, nchan);
     hipLaunchKernelGGL(k_fold, g, dim3(256), 0, (hipStream_t)stream, data, out, ld, npbins, n_fold);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+int pss_fold_periods(const float *data, float *out, int32_t nchan, int64_t ld, int64_t nbin, int64_t nper,
+                     void *stream) {
+    if (nchan <= 0 || nbin < 1 || nper < 1) return fail(PSS_EINVAL, "fold geometry");
+    if (nper * nbin > ld) return fail(PSS_EINVAL, "fold: %lld periods of %lld bins exceed the row", (long long)nper,
+                                      (long long)nbin);
+    dim3 g = stream_grid(nbin, nchan);
+    hipLaunchKernelGGL(k_fold_periods, g, dim3(256), 0, (hipStream_t)stream, data, out, ld, nbin, nper);
     LAUNCHCHK();
     return PSS_OK;
 }

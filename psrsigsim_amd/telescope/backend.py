@@ -45,3 +45,24 @@ class Backend(object):
                                  N_fold, _engine.stream_ptr())
         _lib.check(rc, "fold")
         return out
+
+    def fold_periods(self, signal, pulsar, nbin=None):
+        """Corrected fold (extension; the reference's ``fold`` above is only
+        valid for exactly four periods): the sum of the signal over its whole
+        periods of ``nbin`` samples (default ``int(P * samprate)``, the
+        samples per period make_pulses uses), on the device.  Trailing samples
+        of an incomplete period are dropped.  Returns [Nchan, nbin] float32."""
+        data = signal.data
+        Nf, Nt = data.shape
+        if nbin is None:
+            P = float(to_value(pulsar.period, 's'))
+            nbin = int(P * signal._samprate_MHz() * 1e6)
+        nbin = int(nbin)
+        nper = Nt // nbin if nbin > 0 else 0
+        if nbin < 1 or nper < 1:
+            raise ValueError("fold_periods: %d samples hold no whole period of %d bins" % (Nt, nbin))
+        out = torch.empty((Nf, nbin), dtype=torch.float32, device=data.device)
+        rc = _lib.lib().pss_fold_periods(_engine.ptr(data), _engine.ptr(out), Nf, data.stride(0), nbin, nper,
+                                         _engine.stream_ptr())
+        _lib.check(rc, "fold_periods")
+        return out

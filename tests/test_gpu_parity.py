@@ -121,3 +121,40 @@ def test_c4_fold_mixed_radix_vs_oracle(nchan, null, hip_lib):
     errs = replay.run_case(None, fused=True, case=_c4_case(nchan, null), seed=nchan)
     bad = {k: v for k, v in errs.items() if not v <= TOL}
     assert not bad, errs
+
+
+@pytest.mark.parametrize("nbin,nper,extra", [(244, 17, 5), (1024, 30, 0), (2048, 3, 100)])
+def test_fold_periods_vs_numpy(nbin, nper, extra, hip_lib):
+    """Backend.fold_periods (corrected fold, extension): sum over whole
+    periods = numpy reshape-sum in float64, trailing partial period dropped."""
+    import torch
+    from psrsigsim_amd.telescope import Backend
+
+    class _Sig:
+        def __init__(self, d):
+            self.data = d
+
+    rng = np.random.default_rng(nbin)
+    x = rng.random((3, nbin * nper + extra)).astype(np.float32) * 100
+    out = Backend(samprate=1.0, name="b").fold_periods(_Sig(torch.from_numpy(x).cuda()), None, nbin=nbin)
+    ref = x[:, :nbin * nper].astype(np.float64).reshape(3, nper, nbin).sum(axis=1)
+    np.testing.assert_allclose(out.cpu().numpy(), ref.astype(np.float32), rtol=1e-6)
+
+
+def test_fold_periods_full_c3_size(hip_lib):
+    """At a BASELINE length (2^22 samples, 244-sample periods): the fold of a
+    periodic signal is nper x one period (size-independent property)."""
+    import torch
+    from psrsigsim_amd.telescope import Backend
+
+    class _Sig:
+        def __init__(self, d):
+            self.data = d
+
+    nbin, N = 244, 1 << 22
+    nper = N // nbin
+    one = torch.arange(nbin, dtype=torch.float32, device="cuda") * 0.25
+    x = torch.zeros((2, N), device="cuda")
+    x[:, :nper * nbin] = one.repeat(nper)
+    out = Backend(samprate=1.0, name="b").fold_periods(_Sig(x), None, nbin=nbin)
+    np.testing.assert_array_equal(out.cpu().numpy(), (one.cpu().numpy().astype(np.float64) * nper)[None].repeat(2, 0).astype(np.float32))
