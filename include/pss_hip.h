@@ -149,6 +149,9 @@ int pss_version(void);
  * routes every run through the generic kernels instead of the fast-path
  * specialisations (which must give bitwise identical results). */
 #define PSS_FLAG_NO_FAST 1
+/* PSS_FLAG_DIRECT_DFT sends the fallback lengths N > 8192 through the O(N^2)
+ * direct DFT instead of the Bluestein (chirp-z) path (test hook). */
+#define PSS_FLAG_DIRECT_DFT 2
 int pss_set_flags(int flags);
 int pss_last_error(char *buf, size_t n);
 

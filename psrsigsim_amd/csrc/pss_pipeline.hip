@@ -6,7 +6,9 @@
 //   * no delay stage           : k_elementwise          (1 HBM pass)
 //   * N = 2^m, 64 <= N <= 8192 : k_single<L>            (1 HBM pass, FFT in LDS)
 //   * N = 2^m, N >= 16384      : k_colA -> k_row -> k_colC  (four-step, 2 spills)
-//   * any other even N         : direct DFT fallback    (O(N^2), correctness path)
+//   * 2^m x {6..60} (smooth)   : mixed-radix four-step
+//   * other even N <= 8192     : direct DFT              (O(N^2) in LDS tiles)
+//   * other even N >  8192     : Bluestein chirp-z through a 2^m four-step
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -1458,6 +1460,175 @@ __global__ __launch_bounds__(256) void k_fb_epilogue(KP k) {
 }
 
 // ---------------------------------------------------------------------------
+// path 3b: Bluestein (chirp-z) DFT for the fallback lengths N > 8192 (even N
+// that are neither 2^m nor a mixed-radix split, e.g. the reference's own
+// simulate fixture, 3 125 000 = 2^3 5^8; and delayed nulls on mixed-radix
+// lengths).  With w_n = exp(-pi i n^2 / N) and nk = (n^2 + k^2 - (k-n)^2)/2:
+//     X_k = w_k sum_n (x_n w_n) conj(w_{k-n}),
+// a linear convolution evaluated as a circular one of length
+// M = 2^ceil(log2(2N - 1)) through a power-of-two four-step M = M1 x M2
+// (M2 = 4096, or 8192 for M = 2^25):
+//     col pass  : a_n = x_n w_n (0 for n >= N), FFT over n1, twiddle  -> Z
+//     row pass  : FFT over n2, * Bhat (same permuted order), inverse FFT
+//     col pass  : conj twiddle, inverse FFT over k1, * w_k        -> X
+// Bhat = FFT_M(b)/M, b_m = conj(w_m) for m < N, conj(w_{M-m}) for m > M - N,
+// built by the same col/row kernels (mode 2).  The inverse DFT of the
+// pipeline is conj(DFT(conj X)) / N through the same kernels (mode 1).  Each
+// transform is 3 streaming passes over M complex per channel instead of the
+// direct path's O(N^2); fp32 throughout (relative error ~1e-6 at M = 2^23).
+// ---------------------------------------------------------------------------
+struct BsArgs {
+    const cf *src;     // mode 0/1: complex rows [nchan][N] (the W1 / W2 buffers)
+    cf *dst;           // mode 0/1: complex rows [nchan][N]
+    cf *Z;             // [nb][M] convolution workspace (mode 2: Bhat itself)
+    const cf *chirp;   // [N]  w_n
+    const cf *bhat;    // [M]  permuted order, scaled 1/M
+    int64_t N, M, M1, M2;
+    int r0;            // first channel of this batch
+    int mode;          // 0 forward DFT (+ delay ramp), 1 inverse DFT (/N), 2 Bhat build
+};
+
+// w_n = exp(-pi i n^2 / N): n^2 reduced mod 2N exactly, angle in double
+__global__ void k_bs_chirp(cf *chirp, int64_t N) {
+    for (int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; n < N;
+         n += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t m = ((uint64_t)n * (uint64_t)n) % (uint64_t)(2 * N);
+        double s, c;
+        sincospi(-(double)m / (double)N, &s, &c);
+        chirp[n] = make_float2((float)c, (float)s);
+    }
+}
+
+// exp(sgn 2 pi i m / M), 0 <= m < M <= 2^25: |m| folded to <= M/2, exact in float
+__device__ __forceinline__ cf bs_twiddle(int64_t m, int64_t M, float invM, bool inv) {
+    const int64_t ms = (2 * m > M) ? m - M : m;
+    const float r = (float)ms * invM;
+    return expi_rev(inv ? r : -r);
+}
+
+template <int L, int B, int T, typename R>
+struct BsFft;
+template <int L, int B, int T, int... Rs>
+struct BsFft<L, B, T, RList<Rs...>> {
+    using FF = Fft<L, B, T>;
+    // LDS (natural order, B sequences of L) -> transform -> LDS (natural)
+    template <bool INV>
+    __device__ static __forceinline__ void go(cf *lds, int tid) {
+        cf v[FF::E];
+        FF::template load<FF::template first<Rs...>()>(v, lds, tid);
+        __syncthreads();                // the first stage's scatter rewrites LDS
+        FF::template run<INV, 1, Rs...>(v, lds, tid);
+        __syncthreads();
+        FF::template store<FF::template last_of<Rs...>()>(v, lds, tid);
+        __syncthreads();
+    }
+};
+
+// Column pass over B = 8192 / L adjacent columns n2 (grid: M2 / B, batch rows).
+template <int L, typename R, bool INV>
+__global__ __launch_bounds__(256) void k_bs_col(KP k, BsArgs a) {
+    constexpr int B = 8192 / L, T = 256;
+    __shared__ cf lds[B * Lds<L>::RS];
+    const int tid = threadIdx.x, rb = blockIdx.y, r = a.r0 + rb;
+    const int64_t n20 = (int64_t)blockIdx.x * B;
+    const float invM = 1.0f / (float)a.M;
+    cf *Z = a.Z + (int64_t)rb * a.M;
+    for (int idx = tid; idx < L * B; idx += T) {
+        const int b = idx & (B - 1), n1 = idx / B;
+        const int64_t n = (int64_t)n1 * a.M2 + n20 + b;
+        cf v;
+        if (!INV) {
+            if (a.mode == 2) {
+                const int64_t m = n < a.N ? n : (n > a.M - a.N ? a.M - n : -1);
+                v = m >= 0 ? make_float2(a.chirp[m].x, -a.chirp[m].y) : make_float2(0.f, 0.f);
+            } else if (n < a.N) {
+                cf x = a.src[(int64_t)r * a.N + n];
+                if (a.mode == 1) x.y = -x.y;
+                v = cmul(x, a.chirp[n]);
+            } else {
+                v = make_float2(0.f, 0.f);
+            }
+        } else {
+            // Q[k1 = n1][n2] * exp(+2 pi i n2 k1 / M)
+            v = cmul(Z[n], bs_twiddle((n20 + b) * n1, a.M, invM, true));
+        }
+        lds[Lds<L>::at(b, n1)] = v;
+    }
+    __syncthreads();
+    BsFft<L, B, T, R>::template go<INV>(lds, tid);
+    const float invN = 1.0f / (float)a.N;
+    for (int idx = tid; idx < L * B; idx += T) {
+        const int b = idx & (B - 1), k1 = idx / B;
+        const int64_t n2 = n20 + b, pos = (int64_t)k1 * a.M2 + n2;
+        cf v = lds[Lds<L>::at(b, k1)];
+        if (!INV) {
+            Z[pos] = cmul(v, bs_twiddle(n2 * k1, a.M, invM, false));
+        } else if (pos < a.N) {                 // pos = n1 M2 + n2: output sample / bin
+            v = cmul(v, a.chirp[pos]);
+            if (a.mode == 0) {
+                v = apply_ramp(k, r, pos, v);
+            } else {
+                v = make_float2(v.x * invN, -v.y * invN);
+            }
+            a.dst[(int64_t)r * a.N + pos] = v;
+        }
+    }
+}
+
+// Row pass over one row k1 of M2 (grid: M1, batch rows): forward FFT, then
+// mode 2: scale 1/M and store (Bhat); else * Bhat, inverse FFT, store.
+template <int L, typename F, typename I>
+struct BsRow;
+template <int L, int... F, int... I>
+struct BsRow<L, RList<F...>, RList<I...>> {
+    static constexpr int T = L / 16;
+    using FF = Fft<L, 1, T>;
+    __device__ static void go(const KP &k, const BsArgs &a) {
+        (void)k;
+        __shared__ cf lds[Lds<L>::RS];
+        const int tid = threadIdx.x, k1 = blockIdx.x;
+        cf *row = a.Z + (int64_t)blockIdx.y * a.M + (int64_t)k1 * L;
+        for (int p = tid; p < L; p += T) lds[Lds<L>::at(0, p)] = row[p];
+        __syncthreads();
+        cf v[FF::E];
+        FF::template load<FF::template first<F...>()>(v, lds, tid);
+        __syncthreads();
+        FF::template run<false, 1, F...>(v, lds, tid);
+        constexpr int RFL = FF::template last_of<F...>();
+        constexpr int RIL = FF::template last_of<I...>();
+        if (a.mode == 2) {
+            const float invM = 1.0f / (float)a.M;
+#pragma unroll
+            for (int i = 0; i < FF::E; ++i) {
+                int b, pos;
+                FF::template where<RFL>(i, tid, b, pos);
+                row[pos] = make_float2(v[i].x * invM, v[i].y * invM);
+            }
+            return;
+        }
+        const cf *bh = a.bhat + (int64_t)k1 * L;
+#pragma unroll
+        for (int i = 0; i < FF::E; ++i) {
+            int b, pos;
+            FF::template where<RFL>(i, tid, b, pos);
+            v[i] = cmul(v[i], bh[pos]);
+        }
+        FF::template run<true, 1, I...>(v, lds, tid);
+#pragma unroll
+        for (int i = 0; i < FF::E; ++i) {
+            int b, pos;
+            FF::template where<RIL>(i, tid, b, pos);
+            row[pos] = v[i];
+        }
+    }
+};
+
+template <typename RW>
+__global__ __launch_bounds__(RW::T) void k_bs_row(KP k, BsArgs a) {
+    RW::go(k, a);
+}
+
+// ---------------------------------------------------------------------------
 // utility kernels
 // ---------------------------------------------------------------------------
 __global__ void k_down_sample(const float *in, float *out, int64_t in_len, int64_t in_ld,
@@ -1625,8 +1796,26 @@ static inline bool smooth_split(int64_t n, int64_t *N1 = nullptr, int64_t *N2 = 
     return true;
 }
 
+// Bluestein geometry of a fallback length N > 8192 (path 3b): M = M1 x M2,
+// nb channels per convolution batch (the batch buffer is about one W buffer).
+struct BsGeom { int64_t M, M1, M2, nb; };
+static inline bool bs_len(int64_t N) { return N > 8192 && N <= (1ll << 24); }
+static BsGeom bs_geom(int32_t nchan, int64_t N) {
+    BsGeom g;
+    g.M = 1;
+    while (g.M < 2 * N - 1) g.M <<= 1;
+    g.M2 = g.M >= (1ll << 25) ? 8192 : 4096;
+    g.M1 = g.M / g.M2;
+    g.nb = ((int64_t)nchan * N) / g.M;
+    if (g.nb < 1) g.nb = 1;
+    if (g.nb > nchan) g.nb = nchan;
+    if (g.nb > 65535) g.nb = 65535;
+    return g;
+}
+
 struct WsLayout {
     int64_t yd, mspec, ynode, nodes, bits, base, coef, misc, mbits, rtab, row, total;
+    int64_t bs_chirp, bs_bhat, bs_z;   // Bluestein: w [N] | Bhat [M] | Z [nb][M] (cf)
 };
 
 static WsLayout ws_layout(int32_t nchan, int64_t N) {
@@ -1647,6 +1836,12 @@ static WsLayout ws_layout(int32_t nchan, int64_t N) {
         w.rtab = o;  o += al256((int64_t)nchan * 64 * 8);     // row-pass ramp factors (RFL <= 64)
     } else if (!(is_pow2(N) && N >= 64 && N <= 8192)) {
         o += al256(2 * (int64_t)nchan * N * 8 + N * 8);    // fallback: W1, W2, twiddles
+        if (bs_len(N)) {
+            const BsGeom g = bs_geom(nchan, N);
+            w.bs_chirp = o; o += al256(N * 8);
+            w.bs_bhat = o;  o += al256(g.M * 8);
+            w.bs_z = o;     o += al256(g.nb * g.M * 8);
+        }
         if (smooth_split(N)) {
             // mixed-radix four-step (inside the same bytes: the direct path
             // still serves these lengths for a delayed null)
@@ -1920,7 +2115,102 @@ static int run_single(KP &k, hipStream_t st) {
     return fail(PSS_EUNSUPPORTED, "single-pass: N=%lld", (long long)k.N);
 }
 
+template <int L, typename R>
+static int bs_col(const KP &k, const BsArgs &a, int rows, bool inv, hipStream_t st) {
+    dim3 g((unsigned)(a.M2 / (8192 / L)), (unsigned)rows);
+    if (inv) k_bs_col<L, R, true><<<g, dim3(256), 0, st>>>(k, a);
+    else k_bs_col<L, R, false><<<g, dim3(256), 0, st>>>(k, a);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+static int bs_col_any(const KP &k, const BsArgs &a, int rows, bool inv, hipStream_t st) {
+    switch (a.M1) {
+        case 8:    return bs_col<8, RList<8>>(k, a, rows, inv, st);
+        case 16:   return bs_col<16, RList<16>>(k, a, rows, inv, st);
+        case 32:   return bs_col<32, RList<2, 16>>(k, a, rows, inv, st);
+        case 64:   return bs_col<64, RList<4, 16>>(k, a, rows, inv, st);
+        case 128:  return bs_col<128, RList<8, 16>>(k, a, rows, inv, st);
+        case 256:  return bs_col<256, RList<16, 16>>(k, a, rows, inv, st);
+        case 512:  return bs_col<512, RList<2, 16, 16>>(k, a, rows, inv, st);
+        case 1024: return bs_col<1024, RList<4, 16, 16>>(k, a, rows, inv, st);
+        case 2048: return bs_col<2048, RList<8, 16, 16>>(k, a, rows, inv, st);
+        case 4096: return bs_col<4096, RList<16, 16, 16>>(k, a, rows, inv, st);
+        default: return fail(PSS_EUNSUPPORTED, "Bluestein: M1=%lld", (long long)a.M1);
+    }
+}
+
+static int bs_row_any(const KP &k, const BsArgs &a, int rows, hipStream_t st) {
+    dim3 g((unsigned)a.M1, (unsigned)rows);
+    if (a.M2 == 4096) {
+        using RW = BsRow<4096, RList<16, 16, 16>, RList<16, 16, 16>>;
+        k_bs_row<RW><<<g, dim3(RW::T), 0, st>>>(k, a);
+    } else if (a.M2 == 8192) {
+        using RW = BsRow<8192, RList<16, 16, 16, 2>, RList<2, 16, 16, 16>>;
+        k_bs_row<RW><<<g, dim3(RW::T), 0, st>>>(k, a);
+    } else {
+        return fail(PSS_EUNSUPPORTED, "Bluestein: M2=%lld", (long long)a.M2);
+    }
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+// one Bluestein DFT of every channel row: src -> dst (mode 0 forward + ramp,
+// mode 1 inverse / N), channel batches of nb through the Z buffer
+static int bs_dft(const KP &k, BsArgs a, int64_t nb, hipStream_t st) {
+    for (int64_t r0 = 0; r0 < k.p.nchan; r0 += nb) {
+        const int rows = (int)((k.p.nchan - r0) < nb ? (k.p.nchan - r0) : nb);
+        a.r0 = (int)r0;
+        int rc = bs_col_any(k, a, rows, false, st);
+        if (!rc) rc = bs_row_any(k, a, rows, st);
+        if (!rc) rc = bs_col_any(k, a, rows, true, st);
+        if (rc) return rc;
+    }
+    return PSS_OK;
+}
+
+static int run_bluestein(KP &k, hipStream_t st) {
+    const WsLayout w = ws_layout(k.p.nchan, k.N);
+    const BsGeom g = bs_geom(k.p.nchan, k.N);
+    char *base = reinterpret_cast<char *>(k.p.work);
+    cf *W1 = reinterpret_cast<cf *>(base), *W2 = W1 + (int64_t)k.p.nchan * k.N;
+    BsArgs a;
+    memset(&a, 0, sizeof(a));
+    a.chirp = reinterpret_cast<const cf *>(base + w.bs_chirp);
+    a.bhat = reinterpret_cast<const cf *>(base + w.bs_bhat);
+    a.N = k.N;
+    a.M = g.M;
+    a.M1 = g.M1;
+    a.M2 = g.M2;
+    dim3 ge = stream_grid((k.N + 3) / 4, k.p.nchan);
+    tk_begin(TK_FALLBACK, st);
+    k_fb_source<<<ge, dim3(256), 0, st>>>(k);
+    LAUNCHCHK();
+    k_bs_chirp<<<stream_grid(k.N, 1), dim3(256), 0, st>>>(reinterpret_cast<cf *>(base + w.bs_chirp), k.N);
+    LAUNCHCHK();
+    BsArgs b = a;                       // Bhat: generate b, forward transform, 1/M
+    b.mode = 2;
+    b.Z = reinterpret_cast<cf *>(base + w.bs_bhat);
+    int rc = bs_col_any(k, b, 1, false, st);
+    if (!rc) rc = bs_row_any(k, b, 1, st);
+    if (rc) return rc;
+    a.Z = reinterpret_cast<cf *>(base + w.bs_z);
+    a.src = W1;
+    a.dst = W2;
+    a.mode = 0;
+    if ((rc = bs_dft(k, a, g.nb, st))) return rc;
+    a.src = W2;
+    a.dst = W1;
+    a.mode = 1;
+    if ((rc = bs_dft(k, a, g.nb, st))) return rc;
+    k_fb_epilogue<<<ge, dim3(256), 0, st>>>(k);
+    tk_end(st);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
 static int run_fallback(KP &k, hipStream_t st) {
+    if (bs_len(k.N) && !(g_flags & PSS_FLAG_DIRECT_DFT)) return run_bluestein(k, st);
     dim3 g = stream_grid((k.N + 3) / 4, k.p.nchan);
     tk_begin(TK_FALLBACK, st);
     k_fb_source<<<g, dim3(256), 0, st>>>(k);

@@ -19,6 +19,11 @@ from tests.fixtures_util import load
 
 FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fixtures")
 AMBIG = 1e-3   # |shifted null mask - 1| below which the threshold decision is fp32-ambiguous
+# ... or, at least, the fp32 tolerance (1e-5, north_star) of the transform that
+# carries the mask: paths that pack the mask with the channel's data in one
+# complex row (direct / Bluestein) have an error relative to the larger of the
+# two (a fold-mode channel peaks at ~5000 against a ~120 mask)
+AMBIG_REL = 1e-5
 
 
 def _prof():
@@ -103,6 +108,7 @@ def oracle_exec(case, d):
         elif k == "scatter_conv":
             O.scatter_broaden(sig, op[1], op[2], convolve=True, pulsar=psr)
         elif k == "null":
+            pre_max = np.max(np.abs(np.asarray(sig.data, dtype=np.float64)), axis=1)
             info = O.null(sig, psr, op[1], d)
             inj["null_pulses"] = info["pulses"]
             inj["box"] = info["box_row"]
@@ -111,7 +117,9 @@ def oracle_exec(case, d):
             if info["mask_shifted"] is not None:
                 # samples whose shifted mask is within fp32 reach of the > 1
                 # threshold may legitimately land on either side of it
-                inj["ambiguous"] = np.abs(info["mask_shifted"] - 1.0) < AMBIG
+                ms = np.asarray(info["mask_shifted"], dtype=np.float64)
+                scale = np.maximum(pre_max, np.max(np.abs(ms), axis=1))[:, None]
+                inj["ambiguous"] = np.abs(ms - 1.0) < np.maximum(AMBIG, AMBIG_REL * scale)
         elif k == "observe":
             tel_spec, system, noise = op[1], op[2], op[3]
             if tel_spec == "Arecibo":

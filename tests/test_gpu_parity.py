@@ -24,14 +24,18 @@ def test_golden_replay(name, fused, hip_lib):
 SIZES = [64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536, 1 << 17, 1 << 18,
          1 << 20, 244, 1000, 30720,
          # mixed-radix four-step: N1 x N2 = 6 x 2048, 10 x 4096, 30 x 2048, 30 x 4096, 24 x 8192
-         12288, 40960, 61440, 122880, 196608]
+         12288, 40960, 61440, 122880, 196608,
+         # Bluestein (chirp-z) fallback: M1 x M2 = 8 x 4096 (2 x 5003), 64 x 4096,
+         # 1024 x 4096 (2^20 - 2), 2048 x 4096 (the reference simulate fixture's
+         # 3 125 000 = 2^3 5^8), 4096 x 8192 (2^24 - 2)
+         10006, 100002, (1 << 20) - 2, 3125000, (1 << 24) - 2]
 
 
 @pytest.mark.parametrize("N", SIZES)
 def test_shift_t_rows_vs_oracle(N, hip_lib):
     from psrsigsim_amd.utils import shift_t
     rng = np.random.default_rng(N)
-    R = 3 if N <= (1 << 18) else 1
+    R = 3 if N <= (1 << 18) else (2 if N <= (1 << 22) else 1)
     x = rng.random((R, N)).astype(np.float32)
     shifts = np.array([0.37, -1234.5678, 3.0 * N + 17.25][:R])
     got = shift_t(x, shifts, dt=1.0)
@@ -39,6 +43,24 @@ def test_shift_t_rows_vs_oracle(N, hip_lib):
         ref = O.shift_t(x[r].astype(np.float64), float(shifts[r]), dt=1.0)
         err = np.max(np.abs(got[r] - ref)) / np.max(np.abs(ref))
         assert err < TOL, (N, r, err)
+
+
+@pytest.mark.parametrize("N", [10006, 100002])
+def test_bluestein_matches_direct_dft(N, hip_lib):
+    """The Bluestein path and the O(N^2) direct DFT (PSS_FLAG_DIRECT_DFT) agree
+    on the same rows (both fp32 on the device, direct accumulating in f64)."""
+    from psrsigsim_amd import _lib
+    from psrsigsim_amd.utils import shift_t
+    x = np.random.default_rng(N).random((2, N)).astype(np.float32)
+    s = np.array([12.345, -N / 3.0])
+    a = shift_t(x, s, dt=1.0)
+    L = _lib.load()
+    old = L.pss_set_flags(_lib.FLAG_DIRECT_DFT)
+    try:
+        b = shift_t(x, s, dt=1.0)
+    finally:
+        L.pss_set_flags(old)
+    assert np.max(np.abs(a - b)) / np.max(np.abs(b)) < TOL
 
 
 def test_shift_t_integer_is_roll_full_size(hip_lib):
@@ -119,6 +141,19 @@ def _c4_case(nchan, null):
 @pytest.mark.parametrize("nchan,null", [(3, False), (4, False), (2, True)])
 def test_c4_fold_mixed_radix_vs_oracle(nchan, null, hip_lib):
     errs = replay.run_case(None, fused=True, case=_c4_case(nchan, null), seed=nchan)
+    bad = {k: v for k, v in errs.items() if not v <= TOL}
+    assert not bad, errs
+
+
+@pytest.mark.parametrize("fused", [True, False], ids=["fused", "staged"])
+@pytest.mark.parametrize("N,nchan,null", [(10006, 3, True), (100002, 2, True), (100002, 3, False)])
+def test_bluestein_pipeline_vs_oracle(N, nchan, null, fused, hip_lib):
+    """The whole C3-style chain (scatter convolve, pulses, DM, FD, delayed
+    null, noise) at even lengths with a large prime factor (Bluestein path)
+    against the oracle with injected draws."""
+    case = _big_case(0, nchan, null=null)
+    case["ops"][1] = ("make_pulses", (N + 0.5) * 20.48e-6, "pulses")
+    errs = replay.run_case(None, fused=fused, case=case, seed=N + nchan)
     bad = {k: v for k, v in errs.items() if not v <= TOL}
     assert not bad, errs
 

@@ -78,9 +78,12 @@ def test_save_errors():
 
 
 @pytest.mark.gpu
-def test_simulate_equals_manual_calls(hip_lib):
+@pytest.mark.parametrize("rate", [1.5625, 1.0 * 2048 * 10 ** -6], ids=["fixture", "2048bin"])
+def test_simulate_equals_manual_calls(rate, hip_lib):
     """simulate() = the reference's call sequence (simulate.py:292-326) made
-    by hand with the same seed: bitwise (one fused run either way)."""
+    by hand with the same seed: bitwise (one fused run either way).  The
+    reference fixture's 1.5625 MHz gives 3 125 000 = 2^3 5^8 samples per
+    channel (Bluestein path); the 2048-bin variant is a power of two."""
     import psrsigsim_amd as pss
     from psrsigsim_amd.signal import FilterBankSignal
     from psrsigsim_amd.pulsar import Pulsar, GaussPortrait
@@ -88,9 +91,7 @@ def test_simulate_equals_manual_calls(hip_lib):
     from psrsigsim_amd.telescope import Telescope, Receiver, Backend
     pss.seed(5)
     p = _param_dict()
-    # the reference fixture's 1.5625 MHz gives 3 125 000 = 2^3 5^8 samples, a
-    # length only the O(N^2) direct path takes: use its 2048-bin variant
-    p['sample_rate'] = 1.0 * 2048 * 10 ** -6
+    p['sample_rate'] = rate
     sim = _sim(psrdict=p)
     sim.simulate()
     got = sim.signal.data.cpu().numpy()
