@@ -158,10 +158,15 @@ __device__ __forceinline__ void mask_split(uint64_t w, int L, uint32_t &ishift, 
     t = fmaf((float)(uint32_t)(fr >> 40), 1.1920928955078125e-07f, -1.0f);   // 2 f - 1
 }
 
+__device__ __forceinline__ float cheb_eval_r(const float4 (&q)[3], float t);
 __device__ __forceinline__ float cheb_eval(const float *c, float t) {
-    const float4 a = reinterpret_cast<const float4 *>(c)[0];
-    const float4 b = reinterpret_cast<const float4 *>(c)[1];
-    const float4 d = reinterpret_cast<const float4 *>(c)[2];
+    const float4 q[3] = {reinterpret_cast<const float4 *>(c)[0], reinterpret_cast<const float4 *>(c)[1],
+                         reinterpret_cast<const float4 *>(c)[2]};
+    return cheb_eval_r(q, t);
+}
+// the same Clenshaw evaluation from coefficients already in registers
+__device__ __forceinline__ float cheb_eval_r(const float4 (&q)[3], float t) {
+    const float4 a = q[0], b = q[1], d = q[2];
     const float cc[KCH] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, d.x, d.y, d.z, d.w};
     const float t2 = 2.0f * t;
     float b1 = 0.f, b2 = 0.f;
@@ -210,14 +215,38 @@ __device__ __forceinline__ uint32_t mask_run(const KP &k, uint32_t n, uint32_t i
     const uint32_t msk = RUN >= 32u ? 0xffffffffu : ((1u << RUN) - 1u);
     uint32_t r32 = (uint32_t)(((((uint64_t)Bw.x) << 32) | A.x) >> sh) & msk;
     uint32_t amb = (uint32_t)(((((uint64_t)Bw.y) << 32) | A.y) >> sh) & msk;
+    if (!amb) return r32;
+    // Ambiguous positions cluster at pulse edges (a lane may hold ~20): take
+    // them four at a time so the coefficient loads of a group are in flight
+    // together instead of one exposed latency per position (the table bases
+    // of the two words are loaded once).
+    const uint32_t baseA = k.mt_base[w], baseB = k.mt_base[w2];
     while (amb) {
-        const uint32_t i = (uint32_t)__ffs(amb) - 1u;
-        amb &= amb - 1u;
-        const uint32_t p = (p0 + i) & nm, pw = p >> 5;
-        const uint32_t word = (pw == w) ? A.y : Bw.y;
-        const uint32_t idx = k.mt_base[pw] + (uint32_t)__popc(word & ((1u << (p & 31u)) - 1u));
-        const bool hit = cheb_eval(k.mt_coef + (int64_t)idx * KCH, t) > 1.0f;
-        r32 = (r32 & ~(1u << i)) | ((uint32_t)hit << i);
+        uint32_t ii[4], idx[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            ii[u] = amb ? (uint32_t)__ffs(amb) - 1u : 32u;
+            amb &= amb - 1u;
+            const uint32_t p = (p0 + (ii[u] & 31u)) & nm;
+            const bool inA = (p >> 5) == w;
+            const uint32_t word = inA ? A.y : Bw.y;
+            idx[u] = (inA ? baseA : baseB) + (uint32_t)__popc(word & ((1u << (p & 31u)) - 1u));
+        }
+        float4 c[4][3];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float4 *q = reinterpret_cast<const float4 *>(k.mt_coef + (int64_t)(ii[u] < 32u ? idx[u] : idx[0]) * KCH);
+            c[u][0] = q[0];
+            c[u][1] = q[1];
+            c[u][2] = q[2];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (ii[u] < 32u) {
+                const bool hit = cheb_eval_r(c[u], t) > 1.0f;
+                r32 = (r32 & ~(1u << ii[u])) | ((uint32_t)hit << ii[u]);
+            }
+        }
     }
     return r32;
 }
@@ -289,6 +318,14 @@ __global__ __launch_bounds__(256) void k_null_fix(KP k) {
         const float4 xn = chi2_1x4(gn.bits((uint32_t)(n >> 2), c, (uint32_t)(n >> 34)));
         const float4 xr = chi2_1x4(gr.bits((uint32_t)(n >> 2), c, (uint32_t)(n >> 34)));
         const float vn[4] = {xn.x, xn.y, xn.z, xn.w}, vr[4] = {xr.x, xr.y, xr.z, xr.w};
+        if (h == 15u) {
+            // whole group nulled (the interior of a pulse): one 16-B store
+            // (fast path only: ld % 4 == 0 and a 16-B aligned base)
+            *reinterpret_cast<float4 *>(row + n) =
+                make_float4(fmaf(nn, vn[0], vr[0] * sc), fmaf(nn, vn[1], vr[1] * sc),
+                            fmaf(nn, vn[2], vr[2] * sc), fmaf(nn, vn[3], vr[3] * sc));
+            continue;
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             if ((h >> i) & 1u) row[n + i] = fmaf(nn, vn[i], vr[i] * sc);
