@@ -140,6 +140,18 @@ typedef struct PssPipeline {
        row shifted by the fraction of s_mask; the other
        lengths use `ramp`/`nyq_im` and carry the mask through the FFT.       */
     const uint64_t *mask_ramp;
+
+    /* Baseband path (ISM._disperse_baseband ism/ism.py:76-98,
+       Pulsar._make_amp_pulses pulsar/pulsar.py:153-183).                     */
+    int32_t gen_amp;        /* SEARCH source: sqrt(profile) x N(0,1) draws
+                               (amplitude pulses) instead of profile x chi2   */
+    int32_t reserved0;
+    const float *htab;      /* [nsamp/2 + 1] complex64 transfer function H(k)
+                               of the reference's rfft bins (same for every
+                               row): bin k gets H(k), bin N-k conj H(k), DC
+                               and Nyquist Re H (irfft drops their imaginary
+                               parts).  Non-NULL: replaces the delay ramp and
+                               takes the direct / Bluestein transforms.      */
 } PssPipeline;
 
 /* Library / device info. */
@@ -177,6 +189,14 @@ int pss_run(const PssPipeline *p, void *stream);
  * and the row assignment raises -> PSS_EINVAL).  `nyq` is the Nyquist factor
  * per row (cos(pi*s) for one reference call).  In place.
  */
+/* Filter rows by a per-bin transfer function (baseband coherent dispersion,
+ * ism/ism.py:76-98): rows <- irfft(rfft(row) * H) in place, H = htab
+ * [n/2 + 1] complex64 (interleaved re, im).  Even n <= 2^24.  Workspace:
+ * pss_filter_workspace_bytes(nrows, n). */
+int64_t pss_filter_workspace_bytes(int32_t nrows, int64_t n);
+int pss_filter_rows(float *rows, int32_t nrows, int64_t n, int64_t ld, const float *htab,
+                    void *work, void *stream);
+
 int pss_shift_rows(float *rows, int32_t nrows, int64_t n, int64_t ld,
                    const uint64_t *ramp, const float *nyq, void *work, void *stream);
 

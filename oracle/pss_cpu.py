@@ -53,6 +53,13 @@ class LegacyDraws(object):
         self.log.append(("choice", float(n), np.array(a)))
         return a
 
+    def normal(self, size):
+        """scipy ``norm().rvs(size)`` = ``RandomState.standard_normal``
+        (pulsar.py:166, 183)."""
+        a = self.rs.standard_normal(size)
+        self.log.append(("normal", 0.0, np.array(a)))
+        return a
+
 
 class InjectedDraws(object):
     """Replays a recorded list of (kind, df, array) in order; checks kind, df
@@ -79,6 +86,9 @@ class InjectedDraws(object):
 
     def choice(self, n, k):
         return self._next("choice", n, k)
+
+    def normal(self, size):
+        return self._next("normal", 0.0, size)
 
 
 # ---------------------------------------------------------------------------
@@ -327,6 +337,62 @@ def make_pulses(sig, psr, tobs, draws):
         sig.data = full * draws.chi2(1, (sig.nchan, sig.nsamp)) * sig.draw_norm
     pr = psr.Profiles._max_profile
     sig.Smax = psr.Smean * len(pr) / np.sum(pr)
+
+
+class BasebandSignal(object):
+    """State of a BasebandSignal (signal/bb_signal.py:34-52): Nchan
+    polarisation channels, default sample rate 2 bw (Nyquist)."""
+
+    def __init__(self, fcent, bw, samprate=None, dtype=np.float32, nchan=2):
+        self.fcent = float(fcent)
+        self.bw = float(bw)
+        self.nchan = int(nchan)
+        self.samprate = 2 * self.bw if samprate is None else float(samprate)
+        self.dtype = dtype
+        self.delay = None
+        self.dm = None
+        self.dispersed = False
+        self.data = None
+        self.tobs = self.nsamp = self.Smax = None
+
+
+def make_amp_pulses(sig, psr, tobs, draws):
+    """pulsar.py:107-151 (no spectral index for baseband) + _make_amp_pulses
+    153-183: sqrt(calc_profiles(n / (samprate P) mod 1)) x N(0, 1)."""
+    sig.tobs = float(tobs)
+    if psr.ref_freq is None:
+        psr.ref_freq = sig.fcent
+    Nph = nph_of(sig, psr)
+    psr.Profiles.init_profiles(Nph, sig.nchan)
+    sig.nsamp = int((sig.tobs * sig.samprate) * 1e6)
+    phs = np.arange(sig.nsamp) / ((sig.samprate * psr.period) * 1e6)
+    phs %= 1
+    full = np.sqrt(psr.Profiles.calc(phs, sig.nchan))
+    sig.data = full * draws.normal((sig.nchan, sig.nsamp))
+    pr = psr.Profiles._max_profile
+    sig.Smax = psr.Smean * len(pr) / np.sum(pr)
+
+
+def baseband_transfer(sig, dm, N):
+    """H on the rfft bins of an N-sample row (ism.py:84-93): u =
+    rfftfreq(2 len(rfft) - 1, dt[s]) -- Hz values labelled MHz by
+    make_quant -- f = u - bw/2, H = exp(2 pi i DM_K dm f^2 / ((f + f0)
+    f0^2)), the exponent's MHz s converted to 1e6."""
+    dt_s = (1.0 / sig.samprate) * 1e-6
+    u = np.fft.rfftfreq(2 * (N // 2 + 1) - 1, d=dt_s)
+    f = u - sig.bw / 2.0
+    return np.exp(1j * 2 * np.pi * (DM_K / ((f + sig.fcent) * sig.fcent ** 2) * dm * f ** 2 * 1e6))
+
+
+def disperse_baseband(sig, dm):
+    """ism.py:20-38, 76-98: per channel irfft(rfft(x) H)."""
+    if sig.dispersed:
+        raise ValueError('Signal has already been dispersed!')
+    sig.dm = float(dm)
+    H = baseband_transfer(sig, sig.dm, sig.data.shape[1])
+    for x in range(sig.nchan):
+        sig.data[x] = np.fft.irfft(np.fft.rfft(sig.data[x]) * H)
+    sig.dispersed = True
 
 
 def null(sig, psr, null_frac, draws, length=None, frequency=None):

@@ -176,6 +176,7 @@ class Source(object):
         self.nint = int(nint)
         self.phase_step = int(phase_step)
         self.inj = inj                # global [Nchan, N] draws or None
+        self.amp = False              # amplitude pulses (baseband): sqrt(profile) x N(0,1)
 
 
 class Pending(object):
@@ -206,7 +207,7 @@ def plan_pipeline(sig, pend, rows, chan0):
         P.update(src=_lib.SRC_SEARCH if src.mode == "search" else _lib.SRC_FOLD,
                  prof_rows=src.table.shape[0], nint=src.nint, nph=src.nph,
                  phase_step=src.phase_step, knot_m=src.M, gen_df=src.df,
-                 draw_norm=src.draw_norm, call_gen=src.call_id)
+                 draw_norm=src.draw_norm, call_gen=src.call_id, gen_amp=int(src.amp))
         if src.inj is not None:
             A["inj_gen"] = np.asarray(src.inj, dtype=np.float32)[gidx]
     nul = pend.null
@@ -313,6 +314,19 @@ def execute(sig, pend):
         run(p0, k0)
     p, keep = build_pipeline(sig, pend, rows, sig._c0, sig._buf, out=out)
     run(p, keep)
+
+
+def filter_rows(sig, htab):
+    """rows <- irfft(rfft(row) * H) on the device for every local row of
+    ``sig`` (baseband coherent dispersion, ism.py:76-98); ``htab`` is the
+    complex transfer function on the N/2 + 1 rfft bins."""
+    data = sig.data                                   # flushes pending stages
+    rows, N = data.shape
+    h = to_dev(np.ascontiguousarray(np.asarray(htab, dtype=np.complex64)).view(np.float32))
+    L = _lib.load()
+    ws = workspace(L.pss_filter_workspace_bytes(rows, N))
+    rc = _lib.lib().pss_filter_rows(ptr(data), rows, N, data.stride(0), ptr(h), ptr(ws), stream_ptr())
+    _lib.check(rc, "filter_rows")
 
 
 def probe_row0(sig, pend, count):

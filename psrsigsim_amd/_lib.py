@@ -42,6 +42,7 @@ class PssPipeline(ctypes.Structure):
         ("seed", c_u64), ("call_gen", c_u32), ("call_null", c_u32), ("call_noise", c_u32),
         ("inj_gen", c_vp), ("inj_box", c_vp), ("inj_rep", c_vp), ("inj_noise", c_vp),
         ("mask_ramp", c_vp),
+        ("gen_amp", c_i32), ("reserved0", c_i32), ("htab", c_vp),
     ]
 
 
@@ -55,6 +56,8 @@ EXPORTS = {
                                           ctypes.POINTER(c_i64), ctypes.c_int]),
     "pss_run": (ctypes.c_int, [ctypes.POINTER(PssPipeline), c_vp]),
     "pss_shift_rows": (ctypes.c_int, [c_vp, c_i32, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "pss_filter_workspace_bytes": (c_i64, [c_i32, c_i64]),
+    "pss_filter_rows": (ctypes.c_int, [c_vp, c_i32, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "pss_down_sample": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_vp]),
     "pss_rebin": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp]),
     "pss_clip_cast": (ctypes.c_int, [c_vp, c_vp, c_i64, c_f32, c_i32, c_vp]),

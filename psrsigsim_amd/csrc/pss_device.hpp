@@ -123,6 +123,17 @@ __device__ __forceinline__ float4 chi2_1x4(uint4 r) {
     return make_float4(l0 * c0 * c0, l0 * s0 * s0, l1 * c1 * c1, l1 * s1 * s1);
 }
 
+// Four N(0, 1) draws from one Philox block (Box-Muller pairs
+// sqrt(-2 ln u) (cos 2 pi v, sin 2 pi v)): the amplitude-pulse draws.
+__device__ __forceinline__ float4 normal_x4(uint4 r) {
+    const float l0 = sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01(r.x)));
+    const float l1 = sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01(r.z)));
+    const float v0 = (float)(r.y >> 8) * 5.9604644775390625e-08f;
+    const float v1 = (float)(r.w >> 8) * 5.9604644775390625e-08f;
+    return make_float4(l0 * __builtin_amdgcn_cosf(v0), l0 * __builtin_amdgcn_sinf(v0),
+                       l1 * __builtin_amdgcn_cosf(v1), l1 * __builtin_amdgcn_sinf(v1));
+}
+
 // log1p(y) - y for |y| small, without cancellation (alternating series).
 __device__ __forceinline__ float log1p_minus(float y) {
     if (fabsf(y) < 0.125f) {

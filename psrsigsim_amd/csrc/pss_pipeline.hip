@@ -458,12 +458,21 @@ __device__ __forceinline__ void source4(const KP &k, int r, int64_t n0, int cnt,
                 const float *row = p.inj_gen + (int64_t)r * k.N;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) x[i] = (i < cnt) ? row[n0 + i] : 0.f;
+            } else if (p.gen_amp) {
+                Rng g(p.seed, p.call_gen, P_PULSE);
+                const float4 z = normal_x4(g.bits((uint32_t)(n0 >> 2), c, (uint32_t)(n0 >> 34)));
+                x[0] = z.x; x[1] = z.y; x[2] = z.z; x[3] = z.w;
             } else {
                 Rng g(p.seed, p.call_gen, P_PULSE);
                 draw4(g, n0, c, p.gen_df, x);
             }
             const int prow = (p.prof_rows == 1) ? 0 : (int)c;
-            if (p.src == PSS_SRC_SEARCH) {
+            if (p.src == PSS_SRC_SEARCH && p.gen_amp) {
+                // amplitude pulses: sqrt(calc_profiles(phase)) x N(0, 1)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (i < cnt) re[i] = sqrtf(fmaxf(pchip_eval(k, prow, n0 + i), 0.0f)) * x[i] * p.draw_norm;
+            } else if (p.src == PSS_SRC_SEARCH) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
                     if (i < cnt) re[i] = pchip_eval(k, prow, n0 + i) * x[i] * p.draw_norm;
@@ -579,6 +588,14 @@ __global__ __launch_bounds__(256) void k_box_row(KP k, float *row) {
 __device__ __forceinline__ cf apply_ramp(const KP &k, int r, int64_t kb, cf z) {
     const PssPipeline &p = k.p;
     const int64_t N = k.N;
+    if (p.htab) {
+        // per-bin transfer function of the rfft bins; Hermitian extension,
+        // DC and Nyquist keep Re H only (irfft drops their imaginary parts)
+        const bool upper = 2 * kb > N;
+        const cf h = reinterpret_cast<const cf *>(p.htab)[upper ? N - kb : kb];
+        if (kb == 0 || 2 * kb == N) return make_float2(z.x * h.x, z.y * h.x);
+        return cmul(z, make_float2(h.x, upper ? -h.y : h.y));
+    }
     if (2 * kb == N) return make_float2(z.x * p.nyq_re[r], z.y * p.nyq_im[r]);
     if (kb == 0) return z;
     const int64_t kk = (2 * kb > N) ? kb - N : kb;
@@ -1855,11 +1872,11 @@ struct WsLayout {
     int64_t bs_chirp, bs_bhat, bs_z;   // Bluestein: w [N] | Bhat [M] | Z [nb][M] (cf)
 };
 
-static WsLayout ws_layout(int32_t nchan, int64_t N) {
+static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
     WsLayout w;
     memset(&w, 0, sizeof(w));
     int64_t o = 0;
-    if (fourstep_len(N)) {
+    if (fourstep_len(N) && !filt) {
         const int64_t npairs = ((int64_t)nchan + 2) / 2;   // pairs of (even, odd) global channels
         w.yd = o;    o += al256(npairs * N * 8);
         w.mspec = o; o += al256(N * 8);
@@ -1871,7 +1888,7 @@ static WsLayout ws_layout(int32_t nchan, int64_t N) {
         w.misc = o;  o += 256;
         w.mbits = o; o += al256((int64_t)nchan * (N / 8));   // per-channel null bits
         w.rtab = o;  o += al256((int64_t)nchan * 64 * 8);     // row-pass ramp factors (RFL <= 64)
-    } else if (!(is_pow2(N) && N >= 64 && N <= 8192)) {
+    } else if (filt || !(is_pow2(N) && N >= 64 && N <= 8192)) {
         o += al256(2 * (int64_t)nchan * N * 8 + N * 8);    // fallback: W1, W2, twiddles
         if (bs_len(N)) {
             const BsGeom g = bs_geom(nchan, N);
@@ -1879,7 +1896,7 @@ static WsLayout ws_layout(int32_t nchan, int64_t N) {
             w.bs_bhat = o;  o += al256(g.M * 8);
             w.bs_z = o;     o += al256(g.nb * g.M * 8);
         }
-        if (smooth_split(N)) {
+        if (smooth_split(N) && !filt) {
             // mixed-radix four-step (inside the same bytes: the direct path
             // still serves these lengths for a delayed null)
             const int64_t npairs = ((int64_t)nchan + 2) / 2;
@@ -1899,7 +1916,7 @@ static int g_flags = 0;   // pss_set_flags (test hook)
 
 static bool fast_source(const PssPipeline &p) {
     if (g_flags & PSS_FLAG_NO_FAST) return false;
-    return p.src == PSS_SRC_SEARCH && p.gen_df == 1.0f && !p.inj_gen && p.null_mode != PSS_NULL_UNDELAYED &&
+    return p.src == PSS_SRC_SEARCH && !p.gen_amp && p.gen_df == 1.0f && !p.inj_gen && p.null_mode != PSS_NULL_UNDELAYED &&
            p.nint <= kFastNint;
 }
 static bool fast_epilogue(const KP &k) {
@@ -2207,7 +2224,7 @@ static int bs_dft(const KP &k, BsArgs a, int64_t nb, hipStream_t st) {
 }
 
 static int run_bluestein(KP &k, hipStream_t st) {
-    const WsLayout w = ws_layout(k.p.nchan, k.N);
+    const WsLayout w = ws_layout(k.p.nchan, k.N, k.p.htab != nullptr);
     const BsGeom g = bs_geom(k.p.nchan, k.N);
     char *base = reinterpret_cast<char *>(k.p.work);
     cf *W1 = reinterpret_cast<cf *>(base), *W2 = W1 + (int64_t)k.p.nchan * k.N;
@@ -2285,7 +2302,11 @@ static int validate(const PssPipeline *p) {
     if (p->shift) {
         if (p->nsamp & 1)
             return fail(PSS_EINVAL, "odd N=%lld: the reference's irfft returns N-1 samples", (long long)p->nsamp);
-        if (!p->ramp || !p->nyq_re || !p->nyq_im) return fail(PSS_EINVAL, "shift needs ramp/nyq arrays");
+        if (!p->htab && (!p->ramp || !p->nyq_re || !p->nyq_im))
+            return fail(PSS_EINVAL, "shift needs ramp/nyq arrays");
+        if (p->htab && (p->nsamp > (1ll << 24) || p->null_mode != PSS_NULL_NONE))
+            return fail(PSS_EUNSUPPORTED, "transfer-function run: N=%lld, null %d", (long long)p->nsamp,
+                        p->null_mode);
         if (!p->work) return fail(PSS_EINVAL, "shift needs a workspace");
         if (p->nsamp > (1ll << 24) && !is_pow2(p->nsamp))
             return fail(PSS_EUNSUPPORTED, "N=%lld", (long long)p->nsamp);
@@ -2369,6 +2390,7 @@ int pss_run(const PssPipeline *p, void *stream) {
             row = const_cast<float *>(p->inj_box);
         }
     }
+    if (p->htab) return run_fallback(k, st);        // baseband transfer function
     if (is_pow2(N) && N >= 64 && N <= 8192) return run_single(k, st);
     if (is_pow2(N) && N >= 16384 && N <= (1ll << 24)) return run_fourstep(k, st, row);
     if (smooth_split(N) && p->null_mode != PSS_NULL_DELAYED) return run_smooth(k, st);
@@ -2390,6 +2412,28 @@ int pss_shift_rows(float *rows, int32_t nrows, int64_t n, int64_t ld, const uint
     p.ramp = ramp;
     p.nyq_re = nyq;
     p.nyq_im = nyq;
+    return pss_run(&p, stream);
+}
+
+int64_t pss_filter_workspace_bytes(int32_t nrows, int64_t n) {
+    if (nrows <= 0 || n <= 0) return 0;
+    return ws_layout(nrows, n, true).total;
+}
+
+int pss_filter_rows(float *rows, int32_t nrows, int64_t n, int64_t ld, const float *htab, void *work,
+                    void *stream) {
+    if (!htab) return fail(PSS_EINVAL, "filter_rows: htab is NULL");
+    PssPipeline p;
+    memset(&p, 0, sizeof(p));
+    p.nchan = nrows;
+    p.nsamp = n;
+    p.ld = ld;
+    p.data = rows;
+    p.work = work;
+    p.src = PSS_SRC_LOAD;
+    p.shift = 1;
+    p.data_in_fft = 1;
+    p.htab = htab;
     return pss_run(&p, stream);
 }
 

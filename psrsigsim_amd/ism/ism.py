@@ -66,7 +66,24 @@ class ISM(object):
         push_delay(signal, delays_ms)
 
     def _disperse_baseband(self, signal, dm):
-        raise NotImplementedError("baseband coherent dispersion is outside the filterbank path")
+        """ism.py:76-98: per channel irfft(rfft(x) * H), Lorimer & Kramer
+        (2006) eq. 5.21, H = exp(2 pi i DM_K dm f^2 / ((f + f0) f0^2)), with
+        the reference's frequency grid kept exactly: u = rfftfreq(N + 1, dt)
+        (2 len(rfft) - 1 points) in Hz, labelled MHz by make_quant, f = u -
+        bw/2.  H (N/2 + 1 bins, the same for every channel) is planned on the
+        host in float64; the transforms run on the device."""
+        N = signal._ncols
+        if N % 2:
+            raise ValueError("could not broadcast input array from shape (%d,) into shape (%d,)"
+                             % (N - 1, N))
+        f0 = float(to_value(signal.fcent, 'MHz'))
+        bw = float(to_value(signal.bw, 'MHz'))
+        u = np.fft.rfftfreq(2 * (N // 2 + 1) - 1, d=signal._dt_s())
+        f = u - bw / 2.0
+        # DM_K [MHz^2 s cm^3/pc] dm [pc/cm^3] f^2/((f+f0) f0^2) [1/MHz] -> MHz s = 1e6
+        ph = DM_K_VALUE / ((f + f0) * f0 ** 2) * float(to_value(dm, 'pc/cm^3')) * f ** 2 * 1e6
+        H = np.exp(1j * 2 * np.pi * ph)
+        _engine.filter_rows(signal, H)
 
     def FD_shift(self, signal, FD_params):
         """ism.py:100-156: sum_i FD_i * ln(f / 1 GHz)^(i+1)."""

@@ -84,17 +84,47 @@ class Pulsar(object):
         signal._tobs = make_quant(tobs, 's')
         if self.ref_freq is None:
             self._ref_freq = signal.fcent
-        if signal.sigtype != "FilterBankSignal":
-            raise NotImplementedError("no pulse method for signal: {}".format(signal.sigtype))
-        self._add_spec_idx(signal)
+        if signal.sigtype == "FilterBankSignal":
+            self._add_spec_idx(signal)
         Nph = self._nph(signal)
         self.Profiles.init_profiles(Nph, signal.Nchan)
-        self._make_pow_pulses(signal)
+        if signal.sigtype in ["RFSignal", "BasebandSignal"]:
+            self._make_amp_pulses(signal)
+        elif signal.sigtype == "FilterBankSignal":
+            self._make_pow_pulses(signal)
+        else:
+            raise NotImplementedError("no pulse method for signal: {}".format(signal.sigtype))
         pr = self.Profiles._max_profile
         signal._Smax = self.Smean * len(pr) / np.sum(pr)
 
     def _make_amp_pulses(self, signal):
-        raise NotImplementedError("amplitude (baseband/RF) pulses are outside the filterbank path")
+        """pulsar.py:153-183: data = sqrt(calc_profiles(phase(n))) x N(0, 1),
+        phase(n) = n / (samprate P) mod 1, on the device: the profile's PCHIP
+        table (DataProfile / DataPortrait, as in the reference's own baseband
+        tests) evaluated per sample, Philox Box-Muller normals."""
+        if signal.sigtype != "BasebandSignal":
+            raise NotImplementedError("RFSignal is not built (baseband and filterbank only)")
+        if not hasattr(self.Profiles, "device_table"):
+            raise NotImplementedError(
+                "amplitude pulses need a PCHIP profile (DataProfile / DataPortrait); analytic "
+                "Gaussian profiles are evaluated on the device only through the filterbank path")
+        P = self._P()
+        sr = signal._samprate_MHz()
+        tobs = float(to_value(signal.tobs, 's'))
+        call = _engine.next_call()
+        inj = _engine.take_injection("gen")
+        signal._nsamp = int((tobs * sr) * 1e6)
+        tab, M, nint = self.Profiles.device_table()
+        tab = _dedupe(tab)
+        spp = (sr * P) * 1e6
+        inv = 1.0 / spp
+        step = int(round(math.ldexp(inv - math.floor(inv), 64)))
+        src = _engine.Source("search", tab, 1.0, 1.0, call, M=M, nint=nint, phase_step=step % (1 << 64),
+                             inj=inj)
+        src.amp = True
+        signal._ncols = int(signal._nsamp)
+        signal._pending = _engine.Pending(src)
+        signal._row0 = None
 
     def _make_pow_pulses(self, signal):
         """pulsar.py:185-244: fold -> tile(profiles, nsub) x chi2(Nfold);

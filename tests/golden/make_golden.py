@@ -65,7 +65,17 @@ def _rec_choice(a, size=None, replace=True, p=None):
     return out
 
 
+_orig_norm = _cd.norm_gen._rvs
+
+
+def _rec_norm(self, size=None, random_state=None):
+    out = _orig_norm(self, size=size, random_state=random_state)
+    _DRAWS.append(("normal", 0.0, np.array(out, dtype=np.float64)))
+    return out
+
+
 _cd.chi2_gen._rvs = _rec_rvs
+_cd.norm_gen._rvs = _rec_norm
 np.random.choice = _rec_choice
 
 
@@ -321,7 +331,35 @@ def case_utils():
     c.save()
 
 
+def case_baseband():
+    """Baseband path at the reference's own test
+    geometries: tests/test_ism.py bbsignal (1400 MHz, 400 MHz, 1.024 MHz
+    sampling, 2 pols) with the J1713 DataProfile, P = 5 ms, tobs 0.05 s
+    (51 200 samples), disperse(10); and tests/test_pulsar.py bbsignal
+    (2.048 kHz sampling, P = 1 s, tobs 2 s: 4096 samples), disperse(3)."""
+    from psrsigsim.signal.bb_signal import BasebandSignal
+    c = Case("baseband", 1746)
+    prof = np.load(os.path.join(REF, "psrsigsim/data/J1713+0747_profile.npy"))
+    c.arrays["input_profile"] = np.array(prof, dtype=np.float64)
+    for tag, (sr, per, tobs, dm) in (("a", (500.0 * 2048 * 10 ** -6, 0.005, 0.05, 10.0)),
+                                     ("b", (1.0 * 2048 * 10 ** -6, 1.0, 2.0, 3.0))):
+        sig = BasebandSignal(1400, 400, sample_rate=sr, Nchan=2)
+        psr = Pulsar(per, 10, profiles=DataProfile(prof), name='J1746-0118')
+        psr.make_pulses(sig, tobs)
+        c.snap("pulses_" + tag, sig)
+        c.meta["nsamp_" + tag] = int(sig.nsamp)
+        c.meta["Smax_" + tag] = float(_v(sig._Smax))
+        ISM().disperse(sig, dm)
+        c.snap("disperse_" + tag, sig)
+        c.meta["geom_" + tag] = [sr, per, tobs, dm]
+    c.save()
+
+
 if __name__ == "__main__":
+    if sys.argv[1:]:
+        for name in sys.argv[1:]:
+            globals()["case_" + name]()
+        sys.exit(0)
     case_tutorial1()
     case_northstar_mini()
     case_j1713_search()
@@ -330,3 +368,4 @@ if __name__ == "__main__":
     case_specidx_int8()
     case_observe_branches()
     case_utils()
+    case_baseband()

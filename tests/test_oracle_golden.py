@@ -195,3 +195,32 @@ def test_utils_shift_downsample_rebin():
     close(O.down_sample(A["ds_in"], 4), A["ds_4"], 1e-15)
     for n in (7, 100, 333, 1199):
         close(O.rebin(A["rebin_in"], n), A["rebin_%d" % n], 1e-15)
+
+
+def test_baseband():
+    """Baseband path (§8(f) row 4): amplitude pulses sqrt(PCHIP) x N(0,1)
+    and coherent dispersion irfft(rfft x H) at the reference's own baseband
+    test geometries, injected normal draws."""
+    meta, A, draws = load("baseband")
+    d = O.InjectedDraws(draws)
+    for tag in ("a", "b"):
+        sr, per, tobs, dm = meta["geom_" + tag]
+        sig = O.BasebandSignal(1400, 400, samprate=sr, nchan=2)
+        psr = O.Pulsar(per, 10, profiles=O.DataProfile(A["input_profile"]))
+        O.make_amp_pulses(sig, psr, tobs, d)
+        assert sig.nsamp == meta["nsamp_" + tag]
+        assert np.isclose(sig.Smax, meta["Smax_" + tag], rtol=1e-12)
+        close(sig.data, A["data_pulses_" + tag], 1e-12)
+        # The reference's grid labels Hz as MHz (SURVEY §8 a-row note in
+        # oracle.baseband_transfer), so the phase reaches ~7e10 rad at
+        # geometry a: one float64 ulp of it is ~1e-5 rad, and any change of
+        # operation order (the shim's unit scale included) moves H by that
+        # much.  Tolerance: 4 ulp of the largest phase (b: ~1e-9).
+        dt_s = (1.0 / sr) * 1e-6
+        u = np.fft.rfftfreq(2 * (sig.nsamp // 2 + 1) - 1, d=dt_s)
+        f = u - 200.0
+        maxph = np.max(np.abs(2 * np.pi * O.DM_K / ((f + 1400.0) * 1400.0 ** 2) * dm * f ** 2 * 1e6))
+        O.disperse_baseband(sig, dm)
+        close(sig.data, A["data_disperse_" + tag], max(1e-9, 4 * maxph * 2.0 ** -53))
+        with pytest.raises(ValueError):
+            O.disperse_baseband(sig, dm)
