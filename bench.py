@@ -135,6 +135,48 @@ def cpu_baseline(nch, nsamp_log2):
     return nch * (1 << nsamp_log2) / dt, dt
 
 
+# one all-core worker: bench.cpu_baseline's pipeline on its own channel block
+# (bench.py is not imported there: that would import torch in every worker)
+_ALLCORE_WORKER = r'''
+import sys, time
+sys.path.insert(0, sys.argv[1])
+from oracle import pss_cpu as O
+nch, log2n, seed = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+d = O.LegacyDraws(seed)
+t0 = time.perf_counter()
+sig = O.Signal(1400, 400, nchan=nch, fold=False)
+psr = O.Pulsar(0.005, 1.0, profiles=O.GaussPortrait(0.5, 0.05, 1))
+O.scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
+O.make_pulses(sig, psr, (1 << log2n) * 20.48e-6, d)
+O.disperse(sig, 100)
+O.null(sig, psr, 0.1, d)
+O.observe(sig, psr, O.Arecibo(), "Lband_PUPPI", d, noise=True)
+print(time.perf_counter() - t0)
+'''
+
+
+def cpu_baseline_allcore(workers, nch_each, nsamp_log2):
+    """The same oracle pipeline in ``workers`` concurrent single-threaded
+    processes (one per core, channel blocks of ``nch_each``; the honest
+    all-core CPU figure SURVEY §8(d) asks for next to the single-core one).
+    Child processes (no exec of this GPU process): each times its own
+    pipeline, the job time is the slowest worker."""
+    import subprocess
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    env.pop("HIP_VISIBLE_DEVICES", None)
+    procs = [subprocess.Popen([sys.executable, "-c", _ALLCORE_WORKER, ROOT, str(nch_each),
+                               str(nsamp_log2), str(1776 + w)], stdout=subprocess.PIPE, env=env)
+             for w in range(workers)]
+    times = []
+    for pr in procs:
+        out, _ = pr.communicate(timeout=600)
+        if pr.returncode != 0:
+            raise RuntimeError("all-core CPU worker failed")
+        times.append(float(out.decode().split()[-1]))
+    dt = max(times)
+    return workers * nch_each * (1 << nsamp_log2) / dt, dt
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -154,6 +196,8 @@ def main():
     ap.add_argument("--nchan", type=int, default=NCHAN, help="channels per GPU")
     ap.add_argument("--log2n", type=int, default=LOG2N)
     ap.add_argument("--cpu-chans", type=int, default=8, help="oracle sample size (channels)")
+    ap.add_argument("--cpu-workers", type=int, default=16,
+                    help="all-core CPU baseline: concurrent single-threaded oracle processes (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verbose", action="store_true", help="per-step wall times on stderr")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
@@ -274,8 +318,16 @@ def main():
                 roof["traffic_unit"] = "GB per launch (PMC, profiles/r01/pmc_traffic.json)"
 
     cpu = None
+    cpu_all = None
     if rank == 0 and not args.no_cpu:
         v, dt = cpu_baseline(args.cpu_chans, args.log2n)
+        if args.cpu_workers > 0:
+            va, dta = cpu_baseline_allcore(args.cpu_workers, 2, args.log2n)
+            cpu_all = {"value": round(va, 1), "unit": "channel-samples/s", "cores": args.cpu_workers,
+                       "kind": "port",
+                       "sample": "%d concurrent single-threaded processes x 2 ch x 2^%d samp of the same C3 "
+                                 "pipeline (oracle/pss_cpu.py), slowest worker %.1f s" % (args.cpu_workers,
+                                                                                         args.log2n, dta)}
         cpu = {"value": round(v, 1), "unit": "channel-samples/s", "cores": 1, "kind": "port",
                "sample": "%d ch x 2^%d samp of the same C3 pipeline, oracle/pss_cpu.py (float64 NumPy, "
                          "reference call structure), single process, %.1f s on %s"
@@ -293,6 +345,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "speedup_vs_cpu": round(value / cpu["value"], 1) if cpu else None,
+            "cpu_baseline_allcore": cpu_all,
+            "speedup_vs_cpu_allcore": round(value / cpu_all["value"], 1) if cpu_all else None,
         }
         print(json.dumps(line))
     if world > 1:

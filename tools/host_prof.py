@@ -1,0 +1,28 @@
+"""Host-side profile (cProfile) of a bench workload step on the GPU box:
+where the non-kernel time of a step goes.  usage: tools/host_prof.py c4|c3"""
+import cProfile
+import pstats
+import sys
+import time
+sys.path.insert(0, ".")
+import torch
+import psrsigsim_amd as pss
+import bench
+
+wl = sys.argv[1] if len(sys.argv) > 1 else "c4"
+step = {"c4": lambda: bench.c4_step(pss, 2048, None, False),
+        "c3": lambda: bench.c3_step(pss, 2048, None, 22)}[wl]
+for _ in range(2):
+    s = step()
+    s.data
+torch.cuda.synchronize()
+pr = cProfile.Profile()
+t = time.perf_counter()
+pr.enable()
+for _ in range(5):
+    s = step()
+    s.data
+torch.cuda.synchronize()
+pr.disable()
+print("ms/step %.2f" % ((time.perf_counter() - t) / 5 * 1e3))
+pstats.Stats(pr).sort_stats("tottime").print_stats(25)
