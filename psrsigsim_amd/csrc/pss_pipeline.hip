@@ -1527,9 +1527,11 @@ __global__ __launch_bounds__(256) void k_fb_epilogue(KP k) {
 //     col pass  : conj twiddle, inverse FFT over k1, * w_k        -> X
 // Bhat = FFT_M(b)/M, b_m = conj(w_m) for m < N, conj(w_{M-m}) for m > M - N,
 // built by the same col/row kernels (mode 2).  The inverse DFT of the
-// pipeline is conj(DFT(conj X)) / N through the same kernels (mode 1).  Each
-// transform is 3 streaming passes over M complex per channel instead of the
-// direct path's O(N^2); fp32 throughout (relative error ~1e-6 at M = 2^23).
+// pipeline is conj(DFT(conj X)) / N through the same kernels; the forward
+// DFT's last column pass and the inverse's first share one LDS block (KIND 2),
+// so forward -> ramp -> inverse is 5 streaming passes over M complex per
+// channel instead of the direct path's O(N^2); fp32 throughout (relative
+// error ~2e-6 at M = 2^25).
 // ---------------------------------------------------------------------------
 struct BsArgs {
     const cf *src;     // mode 0/1: complex rows [nchan][N] (the W1 / W2 buffers)
@@ -1579,7 +1581,15 @@ struct BsFft<L, B, T, RList<Rs...>> {
 };
 
 // Column pass over B = 8192 / L adjacent columns n2 (grid: M2 / B, batch rows).
-template <int L, typename R, bool INV>
+// Column pass over B = 8192 / L adjacent columns n2 (grid: M2 / B, batch rows).
+// KIND 0: first pass (a_n = src_n w_n, or b_m for the Bhat build) -> forward
+// FFT -> twiddle -> Z.  KIND 2 (the middle of a forward + inverse DFT pair):
+// conj twiddle -> inverse FFT -> X_n = conv_n w_n, delay ramp / transfer
+// function, then the inverse DFT's input conj(X_n) w_n (0 for n >= N) ->
+// forward FFT -> twiddle -> Z, all in one LDS block (no W2 round trip, one
+// pass fewer).  KIND 1: last pass: conj twiddle -> inverse FFT -> conj(conv_n
+// w_n) / N -> dst.
+template <int L, typename R, int KIND>
 __global__ __launch_bounds__(256) void k_bs_col(KP k, BsArgs a) {
     constexpr int B = 8192 / L, T = 256;
     __shared__ cf lds[B * Lds<L>::RS];
@@ -1587,18 +1597,21 @@ __global__ __launch_bounds__(256) void k_bs_col(KP k, BsArgs a) {
     const int64_t n20 = (int64_t)blockIdx.x * B;
     const float invM = 1.0f / (float)a.M;
     cf *Z = a.Z + (int64_t)rb * a.M;
-    for (int idx = tid; idx < L * B; idx += T) {
+    // loops unrolled (trip counts are compile-time): every load of a thread
+    // in flight together (two 256-thread workgroups per CU leave few waves
+    // to hide HBM latency otherwise)
+#pragma unroll
+    for (int it = 0; it < L * B / T; ++it) {
+        const int idx = tid + it * T;
         const int b = idx & (B - 1), n1 = idx / B;
         const int64_t n = (int64_t)n1 * a.M2 + n20 + b;
         cf v;
-        if (!INV) {
+        if (KIND == 0) {
             if (a.mode == 2) {
                 const int64_t m = n < a.N ? n : (n > a.M - a.N ? a.M - n : -1);
                 v = m >= 0 ? make_float2(a.chirp[m].x, -a.chirp[m].y) : make_float2(0.f, 0.f);
             } else if (n < a.N) {
-                cf x = a.src[(int64_t)r * a.N + n];
-                if (a.mode == 1) x.y = -x.y;
-                v = cmul(x, a.chirp[n]);
+                v = cmul(a.src[(int64_t)r * a.N + n], a.chirp[n]);
             } else {
                 v = make_float2(0.f, 0.f);
             }
@@ -1609,22 +1622,36 @@ __global__ __launch_bounds__(256) void k_bs_col(KP k, BsArgs a) {
         lds[Lds<L>::at(b, n1)] = v;
     }
     __syncthreads();
-    BsFft<L, B, T, R>::template go<INV>(lds, tid);
+    BsFft<L, B, T, R>::template go<KIND != 0>(lds, tid);
+    if (KIND == 2) {
+#pragma unroll
+        for (int it = 0; it < L * B / T; ++it) {
+            const int idx = tid + it * T;
+            const int b = idx & (B - 1), n1 = idx / B;
+            const int64_t pos = (int64_t)n1 * a.M2 + n20 + b;
+            cf v = make_float2(0.f, 0.f);
+            if (pos < a.N) {
+                const cf w = a.chirp[pos];
+                const cf X = apply_ramp(k, r, pos, cmul(lds[Lds<L>::at(b, n1)], w));
+                v = cmul(make_float2(X.x, -X.y), w);
+            }
+            lds[Lds<L>::at(b, n1)] = v;
+        }
+        __syncthreads();
+        BsFft<L, B, T, R>::template go<false>(lds, tid);
+    }
     const float invN = 1.0f / (float)a.N;
-    for (int idx = tid; idx < L * B; idx += T) {
+#pragma unroll
+    for (int it = 0; it < L * B / T; ++it) {
+        const int idx = tid + it * T;
         const int b = idx & (B - 1), k1 = idx / B;
         const int64_t n2 = n20 + b, pos = (int64_t)k1 * a.M2 + n2;
         cf v = lds[Lds<L>::at(b, k1)];
-        if (!INV) {
+        if (KIND != 1) {
             Z[pos] = cmul(v, bs_twiddle(n2 * k1, a.M, invM, false));
-        } else if (pos < a.N) {                 // pos = n1 M2 + n2: output sample / bin
+        } else if (pos < a.N) {                 // pos = n1 M2 + n2: output sample
             v = cmul(v, a.chirp[pos]);
-            if (a.mode == 0) {
-                v = apply_ramp(k, r, pos, v);
-            } else {
-                v = make_float2(v.x * invN, -v.y * invN);
-            }
-            a.dst[(int64_t)r * a.N + pos] = v;
+            a.dst[(int64_t)r * a.N + pos] = make_float2(v.x * invN, -v.y * invN);
         }
     }
 }
@@ -1642,7 +1669,8 @@ struct BsRow<L, RList<F...>, RList<I...>> {
         __shared__ cf lds[Lds<L>::RS];
         const int tid = threadIdx.x, k1 = blockIdx.x;
         cf *row = a.Z + (int64_t)blockIdx.y * a.M + (int64_t)k1 * L;
-        for (int p = tid; p < L; p += T) lds[Lds<L>::at(0, p)] = row[p];
+#pragma unroll
+        for (int i = 0; i < L / T; ++i) lds[Lds<L>::at(0, tid + i * T)] = row[tid + i * T];
         __syncthreads();
         cf v[FF::E];
         FF::template load<FF::template first<F...>()>(v, lds, tid);
@@ -2170,15 +2198,16 @@ static int run_single(KP &k, hipStream_t st) {
 }
 
 template <int L, typename R>
-static int bs_col(const KP &k, const BsArgs &a, int rows, bool inv, hipStream_t st) {
+static int bs_col(const KP &k, const BsArgs &a, int rows, int kind, hipStream_t st) {
     dim3 g((unsigned)(a.M2 / (8192 / L)), (unsigned)rows);
-    if (inv) k_bs_col<L, R, true><<<g, dim3(256), 0, st>>>(k, a);
-    else k_bs_col<L, R, false><<<g, dim3(256), 0, st>>>(k, a);
+    if (kind == 0) k_bs_col<L, R, 0><<<g, dim3(256), 0, st>>>(k, a);
+    else if (kind == 1) k_bs_col<L, R, 1><<<g, dim3(256), 0, st>>>(k, a);
+    else k_bs_col<L, R, 2><<<g, dim3(256), 0, st>>>(k, a);
     LAUNCHCHK();
     return PSS_OK;
 }
 
-static int bs_col_any(const KP &k, const BsArgs &a, int rows, bool inv, hipStream_t st) {
+static int bs_col_any(const KP &k, const BsArgs &a, int rows, int inv, hipStream_t st) {
     switch (a.M1) {
         case 8:    return bs_col<8, RList<8>>(k, a, rows, inv, st);
         case 16:   return bs_col<16, RList<16>>(k, a, rows, inv, st);
@@ -2209,15 +2238,18 @@ static int bs_row_any(const KP &k, const BsArgs &a, int rows, hipStream_t st) {
     return PSS_OK;
 }
 
-// one Bluestein DFT of every channel row: src -> dst (mode 0 forward + ramp,
-// mode 1 inverse / N), channel batches of nb through the Z buffer
-static int bs_dft(const KP &k, BsArgs a, int64_t nb, hipStream_t st) {
+// forward DFT -> delay ramp / transfer function -> inverse DFT / N of every
+// channel row, in place in src, channel batches of nb through the Z buffer:
+// 5 passes over M (first col, row, fused middle col, row, last col)
+static int bs_filter(const KP &k, BsArgs a, int64_t nb, hipStream_t st) {
     for (int64_t r0 = 0; r0 < k.p.nchan; r0 += nb) {
         const int rows = (int)((k.p.nchan - r0) < nb ? (k.p.nchan - r0) : nb);
         a.r0 = (int)r0;
-        int rc = bs_col_any(k, a, rows, false, st);
+        int rc = bs_col_any(k, a, rows, 0, st);
         if (!rc) rc = bs_row_any(k, a, rows, st);
-        if (!rc) rc = bs_col_any(k, a, rows, true, st);
+        if (!rc) rc = bs_col_any(k, a, rows, 2, st);
+        if (!rc) rc = bs_row_any(k, a, rows, st);
+        if (!rc) rc = bs_col_any(k, a, rows, 1, st);
         if (rc) return rc;
     }
     return PSS_OK;
@@ -2227,7 +2259,7 @@ static int run_bluestein(KP &k, hipStream_t st) {
     const WsLayout w = ws_layout(k.p.nchan, k.N, k.p.htab != nullptr);
     const BsGeom g = bs_geom(k.p.nchan, k.N);
     char *base = reinterpret_cast<char *>(k.p.work);
-    cf *W1 = reinterpret_cast<cf *>(base), *W2 = W1 + (int64_t)k.p.nchan * k.N;
+    cf *W1 = reinterpret_cast<cf *>(base);
     BsArgs a;
     memset(&a, 0, sizeof(a));
     a.chirp = reinterpret_cast<const cf *>(base + w.bs_chirp);
@@ -2245,18 +2277,14 @@ static int run_bluestein(KP &k, hipStream_t st) {
     BsArgs b = a;                       // Bhat: generate b, forward transform, 1/M
     b.mode = 2;
     b.Z = reinterpret_cast<cf *>(base + w.bs_bhat);
-    int rc = bs_col_any(k, b, 1, false, st);
+    int rc = bs_col_any(k, b, 1, 0, st);
     if (!rc) rc = bs_row_any(k, b, 1, st);
     if (rc) return rc;
     a.Z = reinterpret_cast<cf *>(base + w.bs_z);
     a.src = W1;
-    a.dst = W2;
-    a.mode = 0;
-    if ((rc = bs_dft(k, a, g.nb, st))) return rc;
-    a.src = W2;
     a.dst = W1;
-    a.mode = 1;
-    if ((rc = bs_dft(k, a, g.nb, st))) return rc;
+    a.mode = 0;
+    if ((rc = bs_filter(k, a, g.nb, st))) return rc;
     k_fb_epilogue<<<ge, dim3(256), 0, st>>>(k);
     tk_end(st);
     LAUNCHCHK();

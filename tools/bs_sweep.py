@@ -1,7 +1,7 @@
 """Diagnostic: Bluestein fallback error per M1 (shift_t vs the float64 oracle)."""
 import sys
 import numpy as np
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from oracle import pss_cpu as O
 from psrsigsim_amd.utils import shift_t
 

@@ -5,7 +5,7 @@ import sys
 import time
 import numpy as np
 import torch
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from psrsigsim_amd import _lib
 from psrsigsim_amd.utils import shift_t
 

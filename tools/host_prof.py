@@ -4,7 +4,7 @@ import cProfile
 import pstats
 import sys
 import time
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 import torch
 import psrsigsim_amd as pss
 import bench
