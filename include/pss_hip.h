@@ -144,7 +144,10 @@ typedef struct PssPipeline {
     /* Baseband path (ISM._disperse_baseband ism/ism.py:76-98,
        Pulsar._make_amp_pulses pulsar/pulsar.py:153-183).                     */
     int32_t gen_amp;        /* SEARCH source: sqrt(profile) x N(0,1) draws
-                               (amplitude pulses) instead of profile x chi2   */
+                               (amplitude pulses) instead of profile x chi2;
+                               1: PCHIP table, 2: analytic Gaussians, prof =
+                               [nint][4] {peak, 1/width, amp/Amax, 0} and
+                               knot_m = 1 (portraits.py:277-290)             */
     int32_t reserved0;
     const float *htab;      /* [nsamp/2 + 1] complex64 transfer function H(k)
                                of the reference's rfft bins (same for every

@@ -207,7 +207,8 @@ def plan_pipeline(sig, pend, rows, chan0):
         P.update(src=_lib.SRC_SEARCH if src.mode == "search" else _lib.SRC_FOLD,
                  prof_rows=src.table.shape[0], nint=src.nint, nph=src.nph,
                  phase_step=src.phase_step, knot_m=src.M, gen_df=src.df,
-                 draw_norm=src.draw_norm, call_gen=src.call_id, gen_amp=int(src.amp))
+                 draw_norm=src.draw_norm, call_gen=src.call_id,
+                 gen_amp=(2 if src.amp == "gauss" else 1) if src.amp else 0)
         if src.inj is not None:
             A["inj_gen"] = np.asarray(src.inj, dtype=np.float32)[gidx]
     nul = pend.null

@@ -437,6 +437,24 @@ __device__ __forceinline__ float pchip_eval(const KP &k, int prow, int64_t n) {
     return pchip_row(k, prow, iv, u);
 }
 
+// Analytic Gaussian portrait at sample n's pulse phase (amplitude pulses of
+// a GaussProfile / 1-D GaussPortrait, portraits.py:143-178, 277-290):
+// prof = [nint components][4] = {peak, 1/width, amp/Amax, 0}, channel
+// independent; the phase is pchip_locate's fraction with knot_m = 1.
+__device__ __forceinline__ float gauss_eval(const KP &k, int64_t n) {
+    uint32_t iv;
+    float u;
+    pchip_locate(k, n, iv, u);
+    const float4 *cp = reinterpret_cast<const float4 *>(k.p.prof);
+    float acc = 0.f;
+    for (int j = 0; j < k.p.nint; ++j) {
+        const float4 c = cp[j];
+        const float d = (u - c.x) * c.y;
+        acc = fmaf(c.z, __expf(-0.5f * d * d), acc);
+    }
+    return acc;
+}
+
 // Source stage for 4 consecutive samples (cnt valid) of local row r.
 // re = data (generated or loaded, with an undelayed null applied);
 // im = delayed-null box mask (0 elsewhere).
@@ -470,8 +488,12 @@ __device__ __forceinline__ void source4(const KP &k, int r, int64_t n0, int cnt,
             if (p.src == PSS_SRC_SEARCH && p.gen_amp) {
                 // amplitude pulses: sqrt(calc_profiles(phase)) x N(0, 1)
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (i < cnt) re[i] = sqrtf(fmaxf(pchip_eval(k, prow, n0 + i), 0.0f)) * x[i] * p.draw_norm;
+                for (int i = 0; i < 4; ++i) {
+                    if (i < cnt) {
+                        const float pr = (p.gen_amp == 2) ? gauss_eval(k, n0 + i) : pchip_eval(k, prow, n0 + i);
+                        re[i] = sqrtf(fmaxf(pr, 0.0f)) * x[i] * p.draw_norm;
+                    }
+                }
             } else if (p.src == PSS_SRC_SEARCH) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)

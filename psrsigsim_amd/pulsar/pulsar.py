@@ -12,6 +12,7 @@ import math
 import numpy as np
 
 from .profiles import GaussProfile, DataPortrait
+from .portraits import GaussPortrait
 from .._units import make_quant, Quantity, to_value
 from .. import _engine
 
@@ -104,24 +105,32 @@ class Pulsar(object):
         tests) evaluated per sample, Philox Box-Muller normals."""
         if signal.sigtype != "BasebandSignal":
             raise NotImplementedError("RFSignal is not built (baseband and filterbank only)")
-        if not hasattr(self.Profiles, "device_table"):
-            raise NotImplementedError(
-                "amplitude pulses need a PCHIP profile (DataProfile / DataPortrait); analytic "
-                "Gaussian profiles are evaluated on the device only through the filterbank path")
         P = self._P()
         sr = signal._samprate_MHz()
         tobs = float(to_value(signal.tobs, 's'))
         call = _engine.next_call()
         inj = _engine.take_injection("gen")
         signal._nsamp = int((tobs * sr) * 1e6)
-        tab, M, nint = self.Profiles.device_table()
-        tab = _dedupe(tab)
         spp = (sr * P) * 1e6
         inv = 1.0 / spp
         step = int(round(math.ldexp(inv - math.floor(inv), 64)))
-        src = _engine.Source("search", tab, 1.0, 1.0, call, M=M, nint=nint, phase_step=step % (1 << 64),
-                             inj=inj)
-        src.amp = True
+        prof = self.Profiles
+        if isinstance(prof, GaussPortrait) and np.ndim(prof.peak) <= 1:
+            # analytic: the device sums the components at each sample's phase
+            pk = np.atleast_1d(np.asarray(prof.peak, dtype=np.float64))
+            wd = np.broadcast_to(np.asarray(prof.width, dtype=np.float64), pk.shape)
+            am = np.broadcast_to(np.asarray(prof.amp, dtype=np.float64), pk.shape)
+            comps = np.stack([pk, 1.0 / wd, am / float(prof.Amax), np.zeros_like(pk)], axis=1)
+            src = _engine.Source("search", comps.astype(np.float32)[None], 1.0, 1.0, call, M=1,
+                                 nint=len(pk), phase_step=step % (1 << 64), inj=inj)
+            src.amp = "gauss"
+        elif hasattr(prof, "device_table"):
+            tab, M, nint = prof.device_table()
+            src = _engine.Source("search", _dedupe(tab), 1.0, 1.0, call, M=M, nint=nint,
+                                 phase_step=step % (1 << 64), inj=inj)
+            src.amp = "pchip"
+        else:
+            raise NotImplementedError("amplitude pulses from a %s" % type(prof).__name__)
         signal._ncols = int(signal._nsamp)
         signal._pending = _engine.Pending(src)
         signal._row0 = None

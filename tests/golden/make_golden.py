@@ -342,9 +342,13 @@ def case_baseband():
     prof = np.load(os.path.join(REF, "psrsigsim/data/J1713+0747_profile.npy"))
     c.arrays["input_profile"] = np.array(prof, dtype=np.float64)
     for tag, (sr, per, tobs, dm) in (("a", (500.0 * 2048 * 10 ** -6, 0.005, 0.05, 10.0)),
-                                     ("b", (1.0 * 2048 * 10 ** -6, 1.0, 2.0, 3.0))):
+                                     ("b", (1.0 * 2048 * 10 ** -6, 1.0, 2.0, 3.0)),
+                                     ("c", (1.024, 0.005, 0.02, 10.0))):
         sig = BasebandSignal(1400, 400, sample_rate=sr, Nchan=2)
-        psr = Pulsar(per, 10, profiles=DataProfile(prof), name='J1746-0118')
+        # c: the default GaussProfile (tests/test_telescope.py::test_bb_obs
+        # makes amplitude pulses with it), at a fixture-sized geometry
+        pro = None if tag == "c" else DataProfile(prof)
+        psr = Pulsar(per, 10, profiles=pro, name='J1746-0118')
         psr.make_pulses(sig, tobs)
         c.snap("pulses_" + tag, sig)
         c.meta["nsamp_" + tag] = int(sig.nsamp)

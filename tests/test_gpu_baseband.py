@@ -26,7 +26,7 @@ def _maxphase(sr, dm, N):
     return float(np.max(np.abs(2 * np.pi * (1.0 / 2.41e-4) / ((f + 1400.0) * 1400.0 ** 2) * dm * f ** 2 * 1e6)))
 
 
-@pytest.mark.parametrize("tag", ["a", "b"])
+@pytest.mark.parametrize("tag", ["a", "b", "c"])
 def test_baseband_golden_exact(tag, hip_lib):
     import psrsigsim_amd as pss
     from psrsigsim_amd.signal import BasebandSignal
@@ -34,9 +34,10 @@ def test_baseband_golden_exact(tag, hip_lib):
     from psrsigsim_amd.ism import ISM
     meta, A, draws = load("baseband")
     sr, per, tobs, dm = meta["geom_" + tag]
-    normal = [a for k, _, a in draws if k == "normal"][0 if tag == "a" else 1]
+    normal = [a for k, _, a in draws if k == "normal"]["abc".index(tag)]
     sig = BasebandSignal(1400, 400, sample_rate=sr, Nchan=2)
-    psr = Pulsar(per, 10, profiles=DataProfile(A["input_profile"]), name='J1746-0118')
+    pro = None if tag == "c" else DataProfile(A["input_profile"])      # c: default GaussProfile
+    psr = Pulsar(per, 10, profiles=pro, name='J1746-0118')
     pss.inject(gen=normal)
     psr.make_pulses(sig, tobs)
     assert sig.nsamp == meta["nsamp_" + tag]
@@ -100,8 +101,6 @@ def test_baseband_errors(hip_lib):
         bb.to_RF()
     with pytest.raises(NotImplementedError):
         bb.to_FilterBank()
-    with pytest.raises(NotImplementedError):
-        Pulsar(1.0, 1.0, profiles=GaussProfile(0.5, 0.05, 1)).make_pulses(bb, 2.0)
     psr = Pulsar(1.0, 1.0, profiles=DataProfile(np.hanning(256) + 0.01))
     odd = BasebandSignal(1400, 400, sample_rate=1.0 * 2048 * 10 ** -6, Nchan=2)
     psr.make_pulses(odd, 2047 / 2048.0 + 1e-9)
@@ -114,3 +113,31 @@ def test_baseband_errors(hip_lib):
     psr.make_pulses(bb, 2.0)
     with pytest.raises(NotImplementedError):
         tel.observe(bb, psr, system="S", noise=False)
+
+
+def test_bb_obs_reference_sequence(hip_lib):
+    """tests/test_telescope.py::test_bb_obs: default-rate BasebandSignal,
+    default GaussProfile pulsar, make_pulses(0.01 s) -- 8e6 samples of
+    amplitude pulses on the device -- then observe raises
+    NotImplementedError; pulses are finite and N(0, prof) shaped."""
+    from psrsigsim_amd.signal import BasebandSignal
+    from psrsigsim_amd.pulsar import Pulsar
+    from psrsigsim_amd.telescope import Telescope, Receiver, Backend
+    from psrsigsim_amd.utils import make_quant
+    bb = BasebandSignal(1400, 400)
+    psr = Pulsar(make_quant(5, 'ms'), 10, name='J1746-0118')
+    tel = Telescope(20.0, area=None, Tsys=25.0, name="Twenty_Meter")
+    tel.add_system(name="Twnty_M", receiver=Receiver(fcent=1400, bandwidth=400, name="Lband"),
+                   backend=Backend(samprate=0.3125, name="Cyborg"))
+    psr.make_pulses(bb, make_quant(0.01, 's'))
+    d = bb.data
+    assert tuple(d.shape) == (2, 8000000)
+    x = d.cpu().numpy()
+    assert np.isfinite(x).all()
+    # phase 0.5 (the Gaussian peak, |x| ~ N(0,1)) vs phase 0 (exp(-50): ~0)
+    spp = 800e6 * 5e-3
+    on = x[:, int(spp * 0.5) - 500: int(spp * 0.5) + 500]
+    off = x[:, :200]
+    assert 0.5 < on.std() < 1.5 and off.std() < 1e-8
+    with pytest.raises(NotImplementedError):
+        tel.observe(bb, psr, system="Twnty_M", noise=False)

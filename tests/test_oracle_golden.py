@@ -203,10 +203,10 @@ def test_baseband():
     test geometries, injected normal draws."""
     meta, A, draws = load("baseband")
     d = O.InjectedDraws(draws)
-    for tag in ("a", "b"):
+    for tag in ("a", "b", "c"):
         sr, per, tobs, dm = meta["geom_" + tag]
         sig = O.BasebandSignal(1400, 400, samprate=sr, nchan=2)
-        psr = O.Pulsar(per, 10, profiles=O.DataProfile(A["input_profile"]))
+        psr = O.Pulsar(per, 10, profiles=None if tag == "c" else O.DataProfile(A["input_profile"]))
         O.make_amp_pulses(sig, psr, tobs, d)
         assert sig.nsamp == meta["nsamp_" + tag]
         assert np.isclose(sig.Smax, meta["Smax_" + tag], rtol=1e-12)
