@@ -319,7 +319,7 @@ def main():
 
     cpu = None
     cpu_all = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:      # contract: CPU baseline at N=1 only
         v, dt = cpu_baseline(args.cpu_chans, args.log2n)
         if args.cpu_workers > 0:
             va, dta = cpu_baseline_allcore(args.cpu_workers, 2, args.log2n)
