@@ -1900,6 +1900,8 @@ static inline bool smooth_split(int64_t n, int64_t *N1 = nullptr, int64_t *N2 = 
     return true;
 }
 
+static int g_flags = 0;   // pss_set_flags (test hook)
+
 // Bluestein geometry of a fallback length N > 8192 (path 3b): M = M1 x M2,
 // nb channels per convolution batch (the batch buffer is about one W buffer).
 struct BsGeom { int64_t M, M1, M2, nb; };
@@ -1939,7 +1941,11 @@ static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
         w.mbits = o; o += al256((int64_t)nchan * (N / 8));   // per-channel null bits
         w.rtab = o;  o += al256((int64_t)nchan * 64 * 8);     // row-pass ramp factors (RFL <= 64)
     } else if (filt || !(is_pow2(N) && N >= 64 && N <= 8192)) {
-        o += al256(2 * (int64_t)nchan * N * 8 + N * 8);    // fallback: W1, W2, twiddles
+        // fallback: W1, W2, twiddles -- Bluestein needs W1 only (its forward
+        // and inverse DFTs are fused through Z), unless the mixed-radix
+        // four-step shares these bytes or the direct DFT is forced
+        const bool w1_only = bs_len(N) && !smooth_split(N) && !(g_flags & PSS_FLAG_DIRECT_DFT);
+        o += al256(w1_only ? (int64_t)nchan * N * 8 : 2 * (int64_t)nchan * N * 8 + N * 8);
         if (bs_len(N)) {
             const BsGeom g = bs_geom(nchan, N);
             w.bs_chirp = o; o += al256(N * 8);
@@ -1962,7 +1968,6 @@ static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
 
 // Fast-path selection (kernels specialised for the north-star configuration;
 // results are bitwise identical to the generic kernels).
-static int g_flags = 0;   // pss_set_flags (test hook)
 
 static bool fast_source(const PssPipeline &p) {
     if (g_flags & PSS_FLAG_NO_FAST) return false;

@@ -44,14 +44,23 @@ def test_workspace_sizes():
     assert L.pss_workspace_bytes(3, n) == 2 * n * 8 + table + 3 * n // 8 + 3 * 512 + n * 4
     sp = 2 * 2 * 244 * 8 + 244 * 8                                   # fallback W1, W2, twiddles
     assert L.pss_workspace_bytes(2, 244) == ((sp + 255) // 256) * 256 + 1024   # row: 976 B, aligned
-    # Bluestein fallback (N > 8192, 2 x 5003): W1, W2, twiddles | chirp [N] |
-    # Bhat [M = 32768] | one batch row [M] (nb = max(1, nchan N / M)) | mask row
+    # Bluestein fallback (N > 8192, 2 x 5003): W1 only (forward and inverse
+    # DFT fused through Z) | chirp [N] | Bhat [M = 32768] | one batch row [M]
+    # (nb = max(1, nchan N / M)) | mask row
     a = lambda b: ((b + 255) // 256) * 256
     n = 10006
-    assert L.pss_workspace_bytes(2, n) == a(5 * n * 8) + a(n * 8) + 2 * a(32768 * 8) + a(n * 4)
-    # 8 x (2^20 - 2): M = 2^22, nb = 8 (2^23 - 16) // 2^22 = 1
+    assert L.pss_workspace_bytes(2, n) == a(2 * n * 8) + a(n * 8) + 2 * a(32768 * 8) + a(n * 4)
+    # 8 x (2^20 - 2): M = 2^22, nb = 8 (2^20 - 2) // 2^21 = 3
     n = (1 << 20) - 2
-    assert L.pss_workspace_bytes(8, n) == a(17 * n * 8) + a(n * 8) + 2 * a((1 << 22) * 8) + a(n * 4)
+    M = 1 << 21
+    assert L.pss_workspace_bytes(8, n) == a(8 * n * 8) + a(n * 8) + a(M * 8) + a(3 * M * 8) + a(n * 4)
+    # the forced direct DFT keeps W1, W2 and the twiddles
+    old = L.pss_set_flags(_lib.FLAG_DIRECT_DFT)
+    try:
+        n = 10006
+        assert L.pss_workspace_bytes(2, n) == a(5 * n * 8) + a(n * 8) + 2 * a(32768 * 8) + a(n * 4)
+    finally:
+        L.pss_set_flags(old)
 
 
 def test_struct_layout_matches_header(tmp_path):
