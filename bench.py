@@ -13,10 +13,21 @@ made signal, through the drop-in API exactly as Simulation.simulate strings it
     Arecibo().observe('Lband_PUPPI', noise=True)
 
 = 2048 x 2^22 channel-samples per GPU, synthetic (Philox) data, fp32 compute.
-Host planning, the channel-0 probe for null's shift_val and the fused device
-run are all inside the timed region.  With --gpus N (torch.distributed, one
-rank per GPU) each rank owns its own 2048-channel block of a 2048*N-channel
-signal (weak scaling; no collective on the data path; shard-invariant RNG).
+Host planning, the channel-0 probe for null's shift_val (on the device, no
+host round trip) and the fused device run are all inside the timed region.
+
+Multi-GPU: one process per GPU over torch.distributed (RCCL).  Under a
+launcher (torchrun / torch.distributed.run: WORLD_SIZE set) every rank runs
+its channel block; invoked directly with --gpus N > 1, bench.py launches the
+N ranks itself (torch.distributed.run as a child process, before anything in
+this process touches the GPU) and exits with their status.
+  --scaling weak   (default): each rank owns its own 2048-channel block of a
+                   2048*N-channel signal (fixed work per GPU);
+  --scaling strong : the BASELINE C3 definition -- ONE 2048-channel signal
+                   split into N contiguous channel blocks (shard.channel_block).
+No collective on the data path (shard-invariant RNG keyed by global channel);
+the timing barrier and the max-over-ranks reduction are the only RCCL calls
+(the C4 workload adds the gather of the folded product).
 
 Reports (one JSON line on rank 0): value = channel-samples/s over all ranks,
 the roofline of the dominant kernel (HIP events on the launch stream, inside
@@ -106,7 +117,27 @@ def c5_step(pss, nchan_total, shard, nsamp_log2):
     return sig
 
 
+def c2_step(pss, nchan_total, shard, nsamp_log2):
+    """BASELINE config C2: NANOGrav L-band search mode, 512 channels x 2^20
+    samples at 20.48 us, J1713+0747 (P = 1/218.81 Hz from the par file, the
+    reference's packaged 2048-bin DataProfile), disperse(DM = 15.917131),
+    GBT Lband_GUPPI radiometer noise."""
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, DataProfile
+    from psrsigsim_amd.ism import ISM
+    from psrsigsim_amd.telescope import telescope as T
+    from psrsigsim_amd.data import j1713_profile
+    sig = FilterBankSignal(1500, 800, Nsubband=nchan_total, sample_rate=0.048828125, fold=False, shard=shard)
+    psr = Pulsar(1.0 / 218.8118437960826270, 0.009, profiles=DataProfile(j1713_profile(), Nchan=nchan_total))
+    psr.make_pulses(sig, tobs=(1 << nsamp_log2) * TOBS_PER_SAMPLE)
+    ISM().disperse(sig, 15.917131)
+    T.GBT().observe(sig, psr, system="Lband_GUPPI", noise=True)
+    return sig
+
+
 WORKLOADS = {
+    "c2": "C2: NANOGrav L-band search mode 512 ch x 2^20 samp per GPU, J1713+0747 DataProfile (P=1/218.81 Hz), "
+          "disperse(DM=15.917131) + GBT Lband_GUPPI radiometer noise",
     "c3": "C3 north-star: FilterBankSignal 2048 ch x 2^22 samp per GPU, GaussProfile P=5 ms, "
           "scatter_broaden(1e-4 s, convolve) + disperse(DM=100) + null(0.1) + Arecibo Lband_PUPPI radiometer noise",
     "c4": "C4: fold mode 2048 ch x (30 subints x 1024 bins) per GPU, P=1/186.49 Hz, disperse(DM=13.3) + "
@@ -114,6 +145,22 @@ WORKLOADS = {
     "c5": "C5 per GPU: 1024 ch x 2^24 samp (8192 ch over 8 GPUs), GaussProfile P=5 ms, disperse(DM=500) + "
           "Arecibo noise",
 }
+
+
+def dry_step(pss, nchan_total, shard, nsamp_log2):
+    """--dry-run: the C3 calls up to the fused run's host plan (no device)."""
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+    from psrsigsim_amd.ism import ISM
+    from psrsigsim_amd import _engine
+    sig = FilterBankSignal(1400, 400, Nsubband=nchan_total, fold=False, shard=shard)
+    psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
+    ism = ISM()
+    ism.scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
+    psr.make_pulses(sig, tobs=(1 << nsamp_log2) * TOBS_PER_SAMPLE)
+    ism.disperse(sig, 100)
+    _engine.plan_pipeline(sig, sig._pending, shard[1] - shard[0], shard[0])
+    return sig
 
 
 def cpu_baseline(nch, nsamp_log2):
@@ -188,9 +235,33 @@ def cpu_model():
     return platform.processor()
 
 
+def _free_port():
+    import socket
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    return port
+
+
+def launch_ranks(n):
+    """Start one rank per GPU (torch.distributed.run, 127.0.0.1) as a child
+    process running this same command line, and return its exit status.
+    Called before this process imports anything that touches the GPU."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+           "--master-addr=127.0.0.1", "--master-port=%d" % _free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: --nchan channels per GPU; strong: --nchan channels in total, split over the GPUs")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU-only check of the launcher / JSON contract: host planning only, gloo, no GPU")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--nchan", type=int, default=NCHAN, help="channels per GPU")
@@ -203,6 +274,13 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
                     help="BASELINE config (default: the north-star C3; c4/c5 are extra measurements)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    if args.workload == "c2":
+        if args.nchan == NCHAN:
+            args.nchan = 512
+        if args.log2n == LOG2N:
+            args.log2n = 20
     if args.workload == "c5":
         if args.nchan == NCHAN:
             args.nchan = 1024
@@ -217,22 +295,39 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        print("bench.py: --gpus %d but the launcher started %d ranks; measuring %d" % (args.gpus, world, world),
+              file=sys.stderr)
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    ranks = dist.get_world_size() if world > 1 else 1
     import psrsigsim_amd as pss
     from psrsigsim_amd import _lib
-    _lib.lib()
+    from psrsigsim_amd.shard import channel_block
+    if not args.dry_run:
+        _lib.lib()
     pss.seed(1776)
 
-    C = args.nchan
-    total = C * world
-    shard = (rank * C, (rank + 1) * C)
+    if args.scaling == "strong":
+        total = args.nchan
+        shard = channel_block(total, rank, world)
+    else:
+        total = args.nchan * world
+        shard = (rank * args.nchan, (rank + 1) * args.nchan)
+    C = shard[1] - shard[0]
+
+    def sync():
+        if not args.dry_run:
+            torch.cuda.synchronize()
 
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        sync()
 
     nsamp = 30720 if args.workload == "c4" else (1 << args.log2n)
 
@@ -243,18 +338,23 @@ def main():
             return _step()
 
     def _step():
+        if args.dry_run:
+            return dry_step(pss, total, shard, args.log2n)
         if args.workload == "c4":
             return c4_step(pss, total, shard, gather=world > 1)
         if args.workload == "c5":
             return c5_step(pss, total, shard, args.log2n)
+        if args.workload == "c2":
+            return c2_step(pss, total, shard, args.log2n)
         return c3_step(pss, total, shard, args.log2n)
 
     for _ in range(args.warmup):
         s = step()
         del s
     barrier()
-    _lib.load().pss_timing_enable(1)
-    _lib.timing_collect()
+    if not args.dry_run:
+        _lib.load().pss_timing_enable(1)
+        _lib.timing_collect()
     t0 = time.perf_counter()
     marks = []
     for _ in range(args.steps):
@@ -263,7 +363,7 @@ def main():
             _ = s.data          # fold-mode output is small: materialise it (the gather did when N > 1)
         del s
         marks.append(time.perf_counter())
-    torch.cuda.synchronize()
+    sync()
     t1 = time.perf_counter()
     if args.verbose:
         prev = t0
@@ -272,11 +372,13 @@ def main():
             prev = m
         print("final sync %.2f ms" % ((t1 - marks[-1]) * 1e3), file=sys.stderr)
     barrier()
-    _lib.load().pss_timing_enable(0)
-    launches = _lib.timing_collect()
+    launches = []
+    if not args.dry_run:
+        _lib.load().pss_timing_enable(0)
+        launches = _lib.timing_collect()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        t = torch.tensor([elapsed], device="cpu" if args.dry_run else "cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     per_step = elapsed / args.steps
@@ -319,7 +421,8 @@ def main():
 
     cpu = None
     cpu_all = None
-    if rank == 0 and world == 1 and not args.no_cpu:      # contract: CPU baseline at N=1 only
+    # CPU baseline: rank 0 at N=1 only, on the C3 pipeline (the metric's workload)
+    if rank == 0 and world == 1 and not args.no_cpu and not args.dry_run and args.workload == "c3":
         v, dt = cpu_baseline(args.cpu_chans, args.log2n)
         if args.cpu_workers > 0:
             va, dta = cpu_baseline_allcore(args.cpu_workers, 2, args.log2n)
@@ -336,10 +439,11 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "channel-samples/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(per_step * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(per_step * 1e3, 3), "higher_is_better": True, "scaling": args.scaling,
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (Philox chi2 pulses/noise)",
-            "config": {"workload": WORKLOADS[args.workload],
+            "config": {"workload": WORKLOADS[args.workload], "nchan_total": total,
                        "nchan_per_gpu": C, "nsamp": nsamp, "parallelism": "channel-shard x%d" % world},
+            "ranks": ranks,
             "gpu_kernel_ms_per_step": round(gpu_ms, 3),
             "kernels": kernels,
             "roofline": roof,
@@ -348,6 +452,8 @@ def main():
             "cpu_baseline_allcore": cpu_all,
             "speedup_vs_cpu_allcore": round(value / cpu_all["value"], 1) if cpu_all else None,
         }
+        if args.dry_run:
+            line["dry_run"] = "host planning only (CPU, gloo): launcher / JSON contract check, not a measurement"
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

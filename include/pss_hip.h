@@ -155,10 +155,15 @@ typedef struct PssPipeline {
                                and Nyquist Re H (irfft drops their imaginary
                                parts).  Non-NULL: replaces the delay ramp and
                                takes the direct / Bluestein transforms.      */
+    const int64_t *null_shift_dev;  /* NULL: use null_shift; else the device
+                               word pss_null_shift wrote (shift_val computed on
+                               the device, no host round trip)                */
 } PssPipeline;
 
 /* Library / device info. */
 int pss_version(void);
+/* "PSS_BUILD_HASH=<sha256 of the sources the library was built from>". */
+const char *pss_build_hash(void);
 
 /* Engine flags (test hook; returns the previous flags).  PSS_FLAG_NO_FAST
  * routes every run through the generic kernels instead of the fast-path
@@ -188,9 +193,10 @@ int pss_run(const PssPipeline *p, void *stream);
 /*
  * utils.shift_t on a batch of rows (utils/utils.py:17-59): every row r is
  * shifted by shift_samples[r] (= shift/dt, may be fractional) through the same
- * FFT engine.  Even N only (odd N: the reference's irfft returns N-1 samples
- * and the row assignment raises -> PSS_EINVAL).  `nyq` is the Nyquist factor
- * per row (cos(pi*s) for one reference call).  In place.
+ * FFT engine.  `nyq` is the Nyquist factor per row (cos(pi*s) for one
+ * reference call; unused for odd N).  In place.  Odd N (3 <= N <= 2^20): the
+ * reference's irfft without n= returns N-1 samples (utils.py:57); they are
+ * written to the first N-1 columns of each row (direct DFTs, f64 sums).
  */
 /* Filter rows by a per-bin transfer function (baseband coherent dispersion,
  * ism/ism.py:76-98): rows <- irfft(rfft(row) * H) in place, H = htab
@@ -248,6 +254,15 @@ int pss_host_ppoly_eval(const double *x, int64_t K, const double *c, int64_t row
                         int64_t n, double *out, int nthreads);
 int pss_host_device_table(const double *c, int64_t rows, int64_t nint, double h, double amax,
                           float *out, int nthreads);
+
+/* Pulsar.null's shift_val (pulsar/pulsar.py:285-288) on the device:
+ *   shift_val = count / 2 - argmax(row[0:count])
+ * out[0] = shift_val (int64), out[1] = status: 0 ok; 1 the maximum is not
+ * unique; 2 a NaN in the row (the reference's np.where then yields 0 or >1
+ * indices and the broadcast raises ValueError).  Stream-ordered, no host
+ * synchronisation: the fused run reads out[0] through
+ * PssPipeline.null_shift_dev. */
+int pss_null_shift(const float *row, int64_t count, int64_t *out, void *stream);
 
 /* Philox chi2 draws (test hook + CPU-independent statistics checks):
  * out[r][n] = chi2(df) keyed like the pipeline's purpose `purpose`. */

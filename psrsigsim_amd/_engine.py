@@ -69,6 +69,26 @@ def inject(**kw):
         _inject[k] = v
 
 
+class RowBlock(object):
+    """Injected per-channel draws for global channels [c0, c0 + len(arr)) only
+    (a shard's rows), instead of a full [Nchan, N] array."""
+
+    def __init__(self, c0, arr):
+        self.c0 = int(c0)
+        self.arr = arr
+
+
+def inj_rows(inj, gidx):
+    """Rows ``gidx`` (global channel indices) of an injected draw array."""
+    if isinstance(inj, RowBlock):
+        rel = np.asarray(gidx) - inj.c0
+        if rel.size and (rel.min() < 0 or rel.max() >= len(inj.arr)):
+            raise KeyError("injected rows cover channels [%d, %d), not %s"
+                           % (inj.c0, inj.c0 + len(inj.arr), list(np.asarray(gidx))))
+        return np.asarray(inj.arr, dtype=np.float32)[rel]
+    return np.asarray(inj, dtype=np.float32)[gidx]
+
+
 def take_injection(kind):
     return _inject.pop(kind, None)
 
@@ -94,8 +114,8 @@ _ws = {}
 
 def workspace(nbytes, role="main"):
     """Cached per-device workspace (grown on demand, never shrunk).  The
-    channel-0 probe has its own (``role="probe"``): it runs on a side stream
-    while the previous main run may still be using the main one."""
+    channel-0 probe of null() has its own (``role="probe"``) so its small run
+    does not resize the main one."""
     dev = device()
     key = (dev.index, role)
     buf = _ws.get(key)
@@ -106,19 +126,6 @@ def workspace(nbytes, role="main"):
         buf = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
         _ws[key] = buf
     return buf
-
-
-_probe_streams = {}
-
-
-def probe_stream():
-    """Side stream of the channel-0 probe (per device)."""
-    dev = device()
-    s = _probe_streams.get(dev.index)
-    if s is None:
-        s = torch.cuda.Stream(device=dev, priority=-1)
-        _probe_streams[dev.index] = s
-    return s
 
 
 def release_workspace():
@@ -210,7 +217,7 @@ def plan_pipeline(sig, pend, rows, chan0):
                  draw_norm=src.draw_norm, call_gen=src.call_id,
                  gen_amp=(2 if src.amp == "gauss" else 1) if src.amp else 0)
         if src.inj is not None:
-            A["inj_gen"] = np.asarray(src.inj, dtype=np.float32)[gidx]
+            A["inj_gen"] = inj_rows(src.inj, gidx)
     nul = pend.null
     need_fft = bool(pend.shifts) or (nul is not None and nul["mode"] == "delayed")
     if need_fft:
@@ -238,7 +245,7 @@ def plan_pipeline(sig, pend, rows, chan0):
         A["nyq_im"] = nyq_im[gidx].astype(np.float32)
     if nul is not None:
         P.update(null_mode=_lib.NULL_DELAYED if nul["mode"] == "delayed" else _lib.NULL_UNDELAYED,
-                 null_slots=int(nul["rank"].size), null_shift=int(nul["shift_val"]),
+                 null_slots=int(nul["rank"].size), null_shift=int(nul.get("shift_val", 0)),
                  nph=int(nul["nph"]), null_box_df=nul["box_df"], null_box_scale=nul["box_scale"],
                  null_rep_df=nul.get("rep_df", 1.0), null_rep_scale=nul.get("rep_scale", 0.0),
                  call_null=nul["call_id"])
@@ -246,12 +253,12 @@ def plan_pipeline(sig, pend, rows, chan0):
         if nul.get("inj_box") is not None:
             A["inj_box"] = np.asarray(nul["inj_box"], dtype=np.float32)
         if nul.get("inj_rep") is not None:
-            A["inj_rep"] = np.asarray(nul["inj_rep"], dtype=np.float32)[gidx]
+            A["inj_rep"] = inj_rows(nul["inj_rep"], gidx)
     noi = pend.noise
     if noi is not None:
         P.update(noise=1, noise_df=noi["df"], noise_norm=noi["norm"], call_noise=noi["call_id"])
         if noi.get("inj") is not None:
-            A["inj_noise"] = np.asarray(noi["inj"], dtype=np.float32)[gidx]
+            A["inj_noise"] = inj_rows(noi["inj"], gidx)
     return P
 
 
@@ -280,6 +287,9 @@ def build_pipeline(sig, pend, rows, chan0, data, out=None, ws_role="main"):
     if P.get("shift"):
         ws = workspace(_lib.load().pss_workspace_bytes(rows, sig._ncols), ws_role)
         p.work = ptr(ws) if ws is not None else None
+    nul = pend.null
+    if nul is not None and nul.get("shift_dev") is not None:
+        p.null_shift_dev = ptr(nul["shift_dev"])
     if out is not None:
         p.out_kind = out["kind"]
         p.out = ptr(out["tensor"])
@@ -311,8 +321,15 @@ def execute(sig, pend):
             if pend.source is None:
                 raise RuntimeError("channel-0 shadow lost")
             sig._row0 = torch.empty((nrow, N), dtype=torch.float32, device=device())
-        p0, k0 = build_pipeline(sig, pend, nrow, 0, sig._row0)
-        run(p0, k0)
+        try:
+            p0, k0 = build_pipeline(sig, pend, nrow, 0, sig._row0)
+        except KeyError:
+            # exact mode with draws injected for this shard's rows only: no
+            # shadow (a later null() on this shard then needs the draws of
+            # channels 0..1, and raises without them)
+            sig._row0 = None
+        else:
+            run(p0, k0)
     p, keep = build_pipeline(sig, pend, rows, sig._c0, sig._buf, out=out)
     run(p, keep)
 
@@ -330,55 +347,57 @@ def filter_rows(sig, htab):
     _lib.check(rc, "filter_rows")
 
 
-def probe_row0(sig, pend, count):
-    """First ``count`` samples of GLOBAL channel 0 after ``pend`` (without
-    noise), on any shard: replayed for global channels 0..1 (the pairing the
-    full run uses, so the values are bit-identical to the final channel 0)
-    from the source when it is generated, else from the local buffer or the
-    channel-0 shadow."""
+def null_shift_device(sig, pend, count):
+    """Pulsar.null's shift_val (pulsar.py:285-288: count//2 - argmax of the
+    first ``count`` samples of GLOBAL channel 0 after ``pend``, without
+    noise) computed on the device, stream-ordered, with no host round trip:
+    returns a device int64 tensor [shift_val, status] (pss_null_shift) that
+    the fused run reads through PssPipeline.null_shift_dev.  Channel 0 is
+    replayed for global channels 0..1 (the pairing the full run uses, so the
+    values are bit-identical to the final channel 0) from the source when it
+    is generated, else taken from the local buffer or the channel-0 shadow --
+    on any shard, without communication."""
     N = sig._ncols
     nrow = min(2, sig.Nchan)
-    main = torch.cuda.current_stream()
-    if pend.source is None:
-        # replaying from existing device data: ordered after the main stream
-        scratch = torch.empty((nrow, N), dtype=torch.float32, device=device())
-        if sig._c0 == 0 and sig._c1 >= nrow:
-            base = sig._buf[0:nrow]
-        else:
-            base = sig._row0
+    if sig._c0 == 0 and sig._c1 >= nrow and sig._buf is not None:
+        base = sig._buf[0:nrow]
+    else:
+        base = sig._row0
+    if pend.empty():
         if base is None:
             raise RuntimeError("no data for channel 0")
-        scratch.copy_(base)
-        side = main
+        row = base[0]
     else:
-        # regenerated from the source: independent of whatever the main
-        # stream is still running (e.g. the previous signal's fused run), so
-        # it goes to a high-priority side stream with its own workspace.
-        # (Measured on MI355X: its kernels still start only after the main
-        # run's big launches drain -- no interleaving -- so what this buys is
-        # that nothing on the host waits for the device except the probe.)
-        side = probe_stream()
-        if getattr(pend.source, "dev_table", None) is not None:
-            side.wait_stream(main)               # table uploaded on the main stream
-    with torch.cuda.stream(side):
-        if pend.source is not None:
-            scratch = torch.empty((nrow, N), dtype=torch.float32, device=device())
+        scratch = torch.empty((nrow, N), dtype=torch.float32, device=device())
+        if pend.source is None:
+            if base is None:
+                raise RuntimeError("no data for channel 0")
+            scratch.copy_(base)
         probe = Pending(pend.source)
         probe.shifts = list(pend.shifts)
         probe.null = pend.null
-        if not probe.empty():
-            p, keep = build_pipeline(sig, probe, nrow, 0, scratch, ws_role="probe")
-            run(p, keep)
-        # pinned, non-blocking read-back + an event on this stream: waits for
-        # the probe only (a pageable .cpu() would wait for the device)
-        row0 = torch.empty(count, dtype=torch.float32, pin_memory=True)
-        row0.copy_(scratch[0, :count], non_blocking=True)
-        done = torch.cuda.Event()
-        done.record(side)
-    done.synchronize()
-    if side is not main:
-        main.wait_stream(side)
-        dt = getattr(pend.source, "dev_table", None)
-        if dt is not None:
-            dt.record_stream(main)
-    return row0.numpy().astype(np.float64)
+        p, keep = build_pipeline(sig, probe, nrow, 0, scratch, ws_role="probe")
+        run(p, keep)
+        row = scratch[0]
+    out = torch.empty(2, dtype=torch.int64, device=device())
+    rc = _lib.lib().pss_null_shift(ptr(row), int(count), ptr(out), stream_ptr())
+    _lib.check(rc, "null_shift")
+    return out
+
+
+def check_null_status(sig):
+    """Raise the reference's error for a null() whose channel-0 maximum was
+    not unique (pulsar.py:286-288: the broadcast of a shift_val of size != 1
+    fails).  Deferred to the first read of the data: the value is on the
+    device, and reading it at null() time would stall the host."""
+    checks = getattr(sig, "_null_checks", None)
+    if not checks:
+        return
+    sig._null_checks = []
+    for t, nph in checks:
+        st = int(t[1].item())
+        if st != 0:
+            raise ValueError("operands could not be broadcast together with shapes (%d,) (%s,)"
+                             % (nph, "0" if st == 2 else "2+"))
+
+

@@ -42,12 +42,13 @@ class PssPipeline(ctypes.Structure):
         ("seed", c_u64), ("call_gen", c_u32), ("call_null", c_u32), ("call_noise", c_u32),
         ("inj_gen", c_vp), ("inj_box", c_vp), ("inj_rep", c_vp), ("inj_noise", c_vp),
         ("mask_ramp", c_vp),
-        ("gen_amp", c_i32), ("reserved0", c_i32), ("htab", c_vp),
+        ("gen_amp", c_i32), ("reserved0", c_i32), ("htab", c_vp), ("null_shift_dev", c_vp),
     ]
 
 
 EXPORTS = {
     "pss_version": (ctypes.c_int, []),
+    "pss_build_hash": (ctypes.c_char_p, []),
     "pss_set_flags": (ctypes.c_int, [ctypes.c_int]),
     "pss_last_error": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
     "pss_workspace_bytes": (c_i64, [c_i32, c_i64]),
@@ -63,6 +64,7 @@ EXPORTS = {
     "pss_clip_cast": (ctypes.c_int, [c_vp, c_vp, c_i64, c_f32, c_i32, c_vp]),
     "pss_fold": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp]),
     "pss_fold_periods": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i64, c_i64, c_i64, c_vp]),
+    "pss_null_shift": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp]),
     "pss_chi2_fill": (ctypes.c_int, [c_vp, c_i32, c_i32, c_i64, c_f32, c_u64, c_u32, c_u32, c_vp]),
     "pss_host_pchip_coef": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, ctypes.c_int]),
     "pss_host_ppoly_eval": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, ctypes.c_int]),
@@ -85,6 +87,8 @@ def load(path=LIB_PATH):
     if not os.path.exists(path):
         raise HipUnavailable("libpss_hip.so not built at %s -- run `python -c 'import "
                              "__graft_entry__ as g; g.build()'`" % path)
+    if path == LIB_PATH and not os.environ.get("PSS_LIB_PATH"):
+        check_build_hash(path)
     L = ctypes.CDLL(path)
     for name, (res, args) in EXPORTS.items():
         fn = getattr(L, name)
@@ -93,6 +97,20 @@ def load(path=LIB_PATH):
     if path == LIB_PATH:
         _LIB = L
     return L
+
+
+def check_build_hash(path=LIB_PATH):
+    """Refuse a library that was not built from the sources in this tree
+    (the hash psrsigsim_amd/build.py compiles into it)."""
+    from . import build as _b
+    try:
+        want = _b.source_hash()
+    except OSError:
+        return          # sources not shipped: nothing to compare against
+    got = _b.embedded_hash(path)
+    if got != want:
+        raise HipUnavailable("%s was built from other sources (hash %s, tree %s) -- rebuild with "
+                             "psrsigsim_amd/build.py" % (path, got, want))
 
 
 def lib():

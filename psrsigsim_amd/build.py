@@ -1,5 +1,14 @@
-"""Build libpss_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+"""Build libpss_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU).
+
+The library embeds the sha256 of its sources (``pss_build_hash``); build()
+recompiles whenever that hash differs from the sources in the tree (content,
+not mtimes: a checkout or a copy to the GPU box can leave a stale binary
+newer than its sources), and ``_lib.load`` refuses a library whose hash does
+not match the sources next to it.
+"""
+import hashlib
 import os
+import re
 import subprocess
 import sys
 
@@ -10,23 +19,42 @@ DEPS = SRC + [os.path.join(HERE, "csrc", f) for f in ("pss_device.hpp", "pss_fft
     [os.path.join(ROOT, "include", "pss_hip.h")]
 OUT = os.path.join(HERE, "libpss_hip.so")
 ARCH = os.environ.get("PSS_OFFLOAD_ARCH", "gfx950")
+# -fno-slp-vectorize: packed f32 (v_pk_*) issues at half rate on gfx950 and
+# costs register-pair moves; scalar f32 is cheaper here.
+FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-slp-vectorize"]
+
+
+def source_hash(extra=()):
+    """sha256 over the library's sources and compile flags."""
+    h = hashlib.sha256()
+    for d in DEPS:
+        with open(d, "rb") as f:
+            h.update(os.path.basename(d).encode() + b"\0" + f.read() + b"\0")
+    h.update(" ".join(list(FLAGS) + list(extra)).encode())
+    return h.hexdigest()
+
+
+def embedded_hash(path=OUT):
+    """The hash string compiled into a built library (read from its bytes,
+    without loading it), or None."""
+    try:
+        with open(path, "rb") as f:
+            m = re.search(rb"PSS_BUILD_HASH=([0-9a-f]{64})", f.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
 
 
 def stale():
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(d) > t for d in DEPS)
+    return embedded_hash() != source_hash()
 
 
 def build(force=False, verbose=True):
     if not force and not stale():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    # -fno-slp-vectorize: packed f32 (v_pk_*) issues at half rate on gfx950 and
-    # costs register-pair moves; scalar f32 is cheaper here.
-    cmd = [hipcc, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-slp-vectorize",
-           "-I" + os.path.join(ROOT, "include"), "-o", OUT + ".tmp"] + SRC
+    cmd = [hipcc] + FLAGS + ['-DPSS_BUILD_HASH="%s"' % source_hash(),
+                             "-I" + os.path.join(ROOT, "include"), "-o", OUT + ".tmp"] + SRC
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

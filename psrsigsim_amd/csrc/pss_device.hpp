@@ -78,9 +78,12 @@ struct Buf {
 // --------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11)
 // --------------------------------------------------------------------------
+#ifndef PSS_PHILOX_ROUNDS
+#define PSS_PHILOX_ROUNDS 10
+#endif
 __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < PSS_PHILOX_ROUNDS; ++r) {
         // one v_mad_u64_u32 per product (hi and lo together), not mul_hi + mul_lo
         const uint64_t p0 = (uint64_t)c.x * 0xD2511F53u;
         const uint64_t p1 = (uint64_t)c.z * 0xCD9E8D57u;
@@ -111,13 +114,24 @@ __device__ __forceinline__ float u01(uint32_t x) {
     return fmaf((float)x, 2.3283064365386963e-10f, 1.1641532182693481e-10f);
 }
 
+// [0, 1) from the top 23 bits of x, by the exponent trick: 1.m - 1 (one
+// shift-or and one subtract, both full rate; v_cvt_f32_u32 issues at half
+// rate on gfx950, tools/probe_rates.hip).  Exact: 23-bit grid of [0, 1).
+__device__ __forceinline__ float frac23(uint32_t x) {
+#ifdef PSS_OLD_CVT   // A/B switch (tools/ablate.sh): the v_cvt form, 24 bits
+    return (float)(x >> 8) * 5.9604644775390625e-08f;
+#else
+    return __uint_as_float(0x3F800000u | (x >> 9)) - 1.0f;
+#endif
+}
+
 // Four chi2(1) draws from one Philox block: z^2 with z Box-Muller normals,
 // -2 ln(u) cos^2(2 pi v) and -2 ln(u) sin^2(2 pi v).
 __device__ __forceinline__ float4 chi2_1x4(uint4 r) {
     float l0 = -1.3862943611198906f * __builtin_amdgcn_logf(u01(r.x));   // -2 ln u = -2 ln2 log2 u
     float l1 = -1.3862943611198906f * __builtin_amdgcn_logf(u01(r.z));
-    float v0 = (float)(r.y >> 8) * 5.9604644775390625e-08f;             // [0,1) revolutions
-    float v1 = (float)(r.w >> 8) * 5.9604644775390625e-08f;
+    float v0 = frac23(r.y);                                              // [0,1) revolutions
+    float v1 = frac23(r.w);
     float c0 = __builtin_amdgcn_cosf(v0), s0 = __builtin_amdgcn_sinf(v0);
     float c1 = __builtin_amdgcn_cosf(v1), s1 = __builtin_amdgcn_sinf(v1);
     return make_float4(l0 * c0 * c0, l0 * s0 * s0, l1 * c1 * c1, l1 * s1 * s1);
@@ -128,8 +142,8 @@ __device__ __forceinline__ float4 chi2_1x4(uint4 r) {
 __device__ __forceinline__ float4 normal_x4(uint4 r) {
     const float l0 = sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01(r.x)));
     const float l1 = sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01(r.z)));
-    const float v0 = (float)(r.y >> 8) * 5.9604644775390625e-08f;
-    const float v1 = (float)(r.w >> 8) * 5.9604644775390625e-08f;
+    const float v0 = frac23(r.y);
+    const float v1 = frac23(r.w);
     return make_float4(l0 * __builtin_amdgcn_cosf(v0), l0 * __builtin_amdgcn_sinf(v0),
                        l1 * __builtin_amdgcn_cosf(v1), l1 * __builtin_amdgcn_sinf(v1));
 }
@@ -174,7 +188,7 @@ __device__ __forceinline__ float chi2_general(const Rng &g, uint32_t a, uint32_t
     for (uint32_t t = 0; t < 64; ++t) {
         uint4 r = g.bits(a, b, t + 1);
         const float l = -1.3862943611198906f * __builtin_amdgcn_logf(u01(r.x));
-        const float z = sqrtf(l) * __builtin_amdgcn_cosf((float)(r.y >> 8) * 5.9604644775390625e-08f);
+        const float z = sqrtf(l) * __builtin_amdgcn_cosf(frac23(r.y));
         const float y = c * z;
         if (y <= -1.0f) continue;
         const float lu = 0.6931471805599453f * __builtin_amdgcn_logf(u01(r.z));

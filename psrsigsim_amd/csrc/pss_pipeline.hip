@@ -41,6 +41,16 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 #define PSS_BC 16
 #define PSS_TC 1024
 #endif
+// cache policy bits of the column passes' spill loads (experiment switch;
+// gfx950 buffer aux: 1 = sc0, 2 = nt, 16 = sc1)
+#ifndef PSS_SPILL_AUX
+#define PSS_SPILL_AUX 0
+#endif
+// fast pass C block width / threads for N = 2^22 on the 512 x 8192 split
+#ifndef PSS_BC8
+#define PSS_BC8 16
+#define PSS_TC8 512
+#endif
 
 
 using namespace pss;
@@ -372,13 +382,14 @@ __device__ __forceinline__ bool box_of(const KP &k, int64_t n, int &rank, int &j
     const PssPipeline &p = k.p;
     rank = -1;
     const int64_t nph = p.nph;
-    int64_t q = n - p.null_shift;
+    const int64_t shift = p.null_shift_dev ? *p.null_shift_dev : p.null_shift;
+    int64_t q = n - shift;
     int64_t s = floordiv(q, nph);
     if (s >= 0 && s < p.null_slots) {
         int r = p.null_rank[s];
         if (r >= 0) { rank = r; j = (int)(q - s * nph); }
     }
-    q = n - k.N - p.null_shift;          // the same sample reached by a negative bin
+    q = n - k.N - shift;                 // the same sample reached by a negative bin
     s = floordiv(q, nph);
     if (s >= 0 && s < p.null_slots) {
         int r = p.null_rank[s];
@@ -418,11 +429,47 @@ __device__ __forceinline__ void pchip_locate(const KP &k, int64_t n, uint32_t &i
     const uint64_t t = (uint64_t)(uint32_t)ph * p.knot_m;
     const uint64_t u64 = (uint64_t)(uint32_t)(ph >> 32) * p.knot_m + (t >> 32);
     iv = (uint32_t)(u64 >> 32);                                    // interval index
-    u = (float)((uint32_t)u64 >> 8) * 5.9604644775390625e-08f;     // fraction, 24 bits
+    u = frac23((uint32_t)u64);                                     // fraction, 23 bits
     if (iv >= (uint32_t)p.nint) {                                  // extrapolate
         u += (float)(iv - (uint32_t)(p.nint - 1));
         iv = p.nint - 1;
     }
+}
+
+// The same (interval, fraction) for consecutive samples by increments: the
+// 96-bit product A(n) = (n phase_step mod 2^64) * knot_m, kept as (lo, u64 =
+// A >> 32), advances by D = phase_step * knot_m; when the phase wraps the
+// interval field comes back by knot_m.  Exact integer arithmetic: bitwise
+// the values pchip_locate computes, at three adds per sample instead of four
+// 32 x 32 -> 64 multiplies.
+struct PhaseWalk {
+    uint32_t lo;
+    uint64_t u64;
+    __device__ __forceinline__ void start(const PssPipeline &p, uint32_t n) {
+        const uint64_t ph = (uint64_t)n * (uint32_t)p.phase_step + ((uint64_t)(n * (uint32_t)(p.phase_step >> 32)) << 32);
+        const uint64_t t = (uint64_t)(uint32_t)ph * p.knot_m;
+        lo = (uint32_t)t;
+        u64 = (uint64_t)(uint32_t)(ph >> 32) * p.knot_m + (t >> 32);
+    }
+    __device__ __forceinline__ void step(uint32_t dlo, uint64_t dhi, uint32_t M) {
+        const uint32_t l2 = lo + dlo;
+        u64 += dhi + (uint64_t)(l2 < lo);
+        lo = l2;
+        if ((uint32_t)(u64 >> 32) >= M) u64 -= (uint64_t)M << 32;
+    }
+    __device__ __forceinline__ void get(const PssPipeline &p, uint32_t &iv, float &u) const {
+        iv = (uint32_t)(u64 >> 32);
+        u = frac23((uint32_t)u64);
+        if (iv >= (uint32_t)p.nint) {
+            u += (float)(iv - (uint32_t)(p.nint - 1));
+            iv = p.nint - 1;
+        }
+    }
+};
+__device__ __forceinline__ void phase_delta(const PssPipeline &p, uint32_t &dlo, uint64_t &dhi) {
+    const uint64_t t = (uint64_t)(uint32_t)p.phase_step * p.knot_m;
+    dlo = (uint32_t)t;
+    dhi = (uint64_t)(uint32_t)(p.phase_step >> 32) * p.knot_m + (t >> 32);
 }
 
 __device__ __forceinline__ float pchip_row(const KP &k, int prow, uint32_t iv, float u) {
@@ -1109,13 +1156,22 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
             const int nint = p.nint;
             const int last = p.prof_rows - 1;
             const int rowa = min(max(pra, 0), last), rowb = min(max(prb, 0), last);
+#ifdef PSS_OLD_PA   // A/B switch (tools/ablate.sh): two table rows, per-sample phase multiplies
+            const bool shared = false;
+#else
+            const bool shared = rowa == rowb;            // one table row for both (e.g. C3's GaussProfile)
+#endif
             const float4 *prof = reinterpret_cast<const float4 *>(p.prof);
             for (int i = tid; i < nint; i += T) {
                 ptab[0][i] = prof[(int64_t)rowa * nint + i];
-                ptab[1][i] = prof[(int64_t)rowb * nint + i];
+                if (!shared) ptab[1][i] = prof[(int64_t)rowb * nint + i];
             }
             __syncthreads();
             const float dn = p.draw_norm;
+            uint32_t dlo;
+            uint64_t dhi;
+            phase_delta(p, dlo, dhi);
+            const uint32_t M = p.knot_m;
 #pragma unroll
             for (int t = 0; t < ITEMS; ++t) {
                 const int it = tid + t * T;
@@ -1125,14 +1181,25 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
                 const float4 qa = chi2_1x4(g.bits(n >> 2, ca, 0u));
                 const float4 qb = chi2_1x4(g.bits(n >> 2, cb, 0u));
                 const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
+                PhaseWalk w;
+                w.start(p, n);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     uint32_t iv;
                     float u;
+#ifdef PSS_OLD_PA
                     pchip_locate(k, (int64_t)(n + (uint32_t)i), iv, u);
-                    const float4 A = ptab[0][iv], Bc = ptab[1][iv];
+#else
+                    if (i) w.step(dlo, dhi, M);
+                    w.get(p, iv, u);
+#endif
+                    const float4 A = ptab[0][iv];
                     const float pa = fmaf(fmaf(fmaf(A.x, u, A.y), u, A.z), u, A.w);
-                    const float pb = fmaf(fmaf(fmaf(Bc.x, u, Bc.y), u, Bc.z), u, Bc.w);
+                    float pb = pa;
+                    if (!shared) {
+                        const float4 Bc = ptab[1][iv];
+                        pb = fmaf(fmaf(fmaf(Bc.x, u, Bc.y), u, Bc.z), u, Bc.w);
+                    }
                     const float xa = pa * va[i] * dn, xb = pb * vb[i] * dn;
                     lds[Lds<N1>::at(b4 + i, n1)] = make_float2(hasa ? xa : 0.f, hasb ? xb : 0.f);
                 }
@@ -1225,7 +1292,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
                 off = (uint32_t)it * 32u;
                 so = (uint32_t)n20 * (uint32_t)(N1 * 8);
             }
-            const float4 lo = Y.ld4(off, so), hi = Y.ld4(off + 16u, so);
+            const float4 lo = Y.ld4<PSS_SPILL_AUX>(off, so), hi = Y.ld4<PSS_SPILL_AUX>(off + 16u, so);
             const cf a[4] = {make_float2(lo.x, lo.y), make_float2(lo.z, lo.w),
                              make_float2(hi.x, hi.y), make_float2(hi.z, hi.w)};
             // W^{m}, m = (n20 + b4 + i) k1 < N (exact in 32-bit and float):
@@ -1389,6 +1456,7 @@ __global__ __launch_bounds__(T) void k_pairC_fast(KP k) { C::passC_fast(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_node_col(KP k, float *nodes) { C::node_col(k, nodes); }
 
+
 // Node ramps of the mask table: f_j = (t_j + 1)/2 at the Chebyshev points
 // t_j = cos(pi (j + 1/2) / KCH); ramp word f_j / N * 2^64, Nyquist cos(pi f_j).
 __global__ void k_node_params(uint64_t *ramp, float *nyq, int L) {
@@ -1533,6 +1601,48 @@ __global__ __launch_bounds__(256) void k_fb_epilogue(KP k) {
         for (int i = 0; i < cnt; ++i) { pre[i] = W1[n0 + i].x; msk[i] = W1[n0 + i].y; }
         epilogue4(k, r, n0, cnt, pre, msk, !re_in);
     }
+}
+
+// ---------------------------------------------------------------------------
+// odd N (utils.shift_t only): the reference's irfft without n= returns
+// L = N - 1 samples -- the inverse of length L of the N-point spectrum's bins
+// 0..M (M = (N - 1)/2), bin M taken as L's Nyquist bin (real part only):
+//   y_m = (Re X_0 + 2 sum_{0<k<M} Re(X_k e^{2 pi i k m / L}) + Re X_M (-1)^m) / L
+// with X = rfft(y) * ramp (utils.py:52-57).  Direct O(N^2) sums, f64
+// accumulation, after the forward direct DFT (k_fb_dft<false>) into W2.
+// ---------------------------------------------------------------------------
+__global__ void k_odd_twiddles(cf *tw, int64_t L) {
+    for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < L; m += (int64_t)gridDim.x * blockDim.x) {
+        double s, c;
+        sincospi(2.0 * (double)m / (double)L, &s, &c);
+        tw[m] = make_float2((float)c, (float)s);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_odd_irfft(KP k, const cf *tw, float *rows, int64_t ld) {
+    __shared__ cf tile[1024];
+    const int r = blockIdx.y;
+    const int64_t N = k.N, L = N - 1, M = L / 2;
+    const cf *X = reinterpret_cast<const cf *>(k.p.work) + (int64_t)(k.p.nchan + r) * N;
+    const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t mm = m < L ? m : 0;
+    double acc = 0.0;
+    for (int64_t base = 1; base < M; base += 1024) {
+        const int cnt = (int)min((int64_t)1024, M - base);
+        __syncthreads();
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x) tile[i] = X[base + i];
+        __syncthreads();
+        int64_t j = (base * mm) % L;               // twiddle index (k m) mod L, advanced exactly
+        for (int i = 0; i < cnt; ++i) {
+            const cf w = tw[j], x = tile[i];
+            acc += (double)x.x * w.x - (double)x.y * w.y;
+            j += mm;
+            if (j >= L) j -= L;
+        }
+    }
+    if (m >= L) return;
+    const double ends = (double)X[0].x + ((m & 1) ? -(double)X[M].x : (double)X[M].x);
+    rows[(int64_t)r * ld + m] = (float)((ends + 2.0 * acc) / (double)L);
 }
 
 // ---------------------------------------------------------------------------
@@ -1805,6 +1915,38 @@ __global__ void k_fold_periods(const float *data, float *out, int64_t ld, int64_
     }
 }
 
+// shift_val = count/2 - argmax(row[0:count]) with the reference's failure
+// cases flagged (non-unique maximum, NaN); one workgroup
+__global__ __launch_bounds__(256) void k_null_shift(const float *row, int64_t count, int64_t *out) {
+    __shared__ float smax[256];
+    __shared__ int sidx[256], scnt[256], snan[256];
+    float m = -INFINITY;
+    int idx = -1, cnt = 0, nan = 0;
+    for (int64_t i = threadIdx.x; i < count; i += 256) {
+        const float v = row[i];
+        if (v != v) { nan = 1; continue; }
+        if (v > m) { m = v; idx = (int)i; cnt = 1; }
+        else if (v == m) { ++cnt; }
+    }
+    smax[threadIdx.x] = m;
+    sidx[threadIdx.x] = idx;
+    scnt[threadIdx.x] = cnt;
+    snan[threadIdx.x] = nan;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float M = -INFINITY;
+        int I = -1, C = 0, Nn = 0;
+        for (int t = 0; t < 256; ++t) {
+            Nn |= snan[t];
+            if (scnt[t] == 0) continue;
+            if (smax[t] > M) { M = smax[t]; I = sidx[t]; C = scnt[t]; }
+            else if (smax[t] == M) { C += scnt[t]; if (sidx[t] < I) I = sidx[t]; }
+        }
+        out[0] = count / 2 - (int64_t)(I < 0 ? 0 : I);
+        out[1] = Nn ? 2 : (C != 1 ? 1 : 0);
+    }
+}
+
 __global__ void k_chi2_fill(float *out, int64_t n, int32_t chan0, float df, uint64_t seed,
                             uint32_t call_id, uint32_t purpose) {
     const int r = blockIdx.y;
@@ -1922,6 +2064,7 @@ static BsGeom bs_geom(int32_t nchan, int64_t N) {
 struct WsLayout {
     int64_t yd, mspec, ynode, nodes, bits, base, coef, misc, mbits, rtab, row, total;
     int64_t bs_chirp, bs_bhat, bs_z;   // Bluestein: w [N] | Bhat [M] | Z [nb][M] (cf)
+    int64_t odd_tw;                    // odd N: exp(+2 pi i j / (N - 1)), j < N - 1 (cf)
 };
 
 static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
@@ -1944,9 +2087,14 @@ static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
         // fallback: W1, W2, twiddles -- Bluestein needs W1 only (its forward
         // and inverse DFTs are fused through Z), unless the mixed-radix
         // four-step shares these bytes or the direct DFT is forced
-        const bool w1_only = bs_len(N) && !smooth_split(N) && !(g_flags & PSS_FLAG_DIRECT_DFT);
+        const bool odd = (N & 1) != 0;
+        const bool w1_only = bs_len(N) && !odd && !smooth_split(N) && !(g_flags & PSS_FLAG_DIRECT_DFT);
         o += al256(w1_only ? (int64_t)nchan * N * 8 : 2 * (int64_t)nchan * N * 8 + N * 8);
-        if (bs_len(N)) {
+        if (odd) {
+            // odd-length shift_t: twiddles of the (N - 1)-point inverse
+            w.odd_tw = o;
+            o += al256((N - 1) * 8);
+        } else if (bs_len(N)) {
             const BsGeom g = bs_geom(nchan, N);
             w.bs_chirp = o; o += al256(N * 8);
             w.bs_bhat = o;  o += al256(g.M * 8);
@@ -2131,6 +2279,13 @@ static int run_fourstep(KP &k, hipStream_t st, const float *mask_row) {
         k.N2 = 4096;
         k.N1 = 1024;
         return launch_pair<1024, 8, 512, C1kF, C1kF, 4096, 512, C4k, C4k, 256, PSS_BC, PSS_TC>(k, st, mask_row);
+    }
+    if (N == (1 << 22)) {
+        // 512 x 8192 split (layout experiment; the 1024 x 4096 split above is
+        // the product default)
+        k.N2 = 8192;
+        k.N1 = 512;
+        return launch_pair<512, 16, 512, C512F, C512F, 8192, 1024, C8kF, C8kI, 512, PSS_BC8, PSS_TC8>(k, st, mask_row);
     }
     if (N == (1 << 24)) {
         // C5 rows: 2048 x 8192; the fast pass C takes 8 columns per workgroup
@@ -2376,6 +2531,13 @@ extern "C" {
 
 int pss_version(void) { return 100; }
 
+// sha256 of the library's sources (psrsigsim_amd/build.py), so a loader can
+// tell whether this binary was built from the sources next to it
+#ifndef PSS_BUILD_HASH
+#define PSS_BUILD_HASH "unknown"
+#endif
+const char *pss_build_hash(void) { return "PSS_BUILD_HASH=" PSS_BUILD_HASH; }
+
 int pss_set_flags(int flags) {
     const int old = g_flags;
     g_flags = flags;
@@ -2452,8 +2614,51 @@ int pss_run(const PssPipeline *p, void *stream) {
     return run_fallback(k, st);
 }
 
+// odd n: forward N-point direct DFT x ramp, then the (N - 1)-point inverse
+static int shift_rows_odd(float *rows, int32_t nrows, int64_t n, int64_t ld, const uint64_t *ramp, void *work,
+                          hipStream_t st) {
+    if (n < 3) return fail(PSS_EINVAL, "shift_t: invalid number of data points (%lld) for the inverse", (long long)(n - 1));
+    if (!ramp || !work || !rows) return fail(PSS_EINVAL, "shift_t: NULL argument");
+    if (nrows > 65535) return fail(PSS_EINVAL, "nchan %d > 65535 per launch", nrows);
+    KP k;
+    memset(&k, 0, sizeof(k));
+    k.p.nchan = nrows;
+    k.p.nsamp = n;
+    k.p.ld = ld;
+    k.p.data = rows;
+    k.p.work = work;
+    k.p.src = PSS_SRC_LOAD;
+    k.p.shift = 1;
+    k.p.data_in_fft = 1;
+    k.p.ramp = ramp;
+    k.N = n;
+    k.N1 = 1;
+    k.N2 = n;
+    const WsLayout w = ws_layout(nrows, n);
+    cf *tw = reinterpret_cast<cf *>(reinterpret_cast<char *>(work) + w.odd_tw);
+    dim3 g = stream_grid((n + 3) / 4, nrows);
+    k_fb_source<<<g, dim3(256), 0, st>>>(k);
+    LAUNCHCHK();
+    k_fb_twiddles<<<stream_grid(n, 1), dim3(256), 0, st>>>(k);
+    LAUNCHCHK();
+    k_odd_twiddles<<<stream_grid(n - 1, 1), dim3(256), 0, st>>>(tw, n - 1);
+    LAUNCHCHK();
+    // only bins 0..M of the forward transform are used
+    const int64_t M = (n - 1) / 2;
+    k_fb_dft<false><<<dim3((unsigned)((M + 1 + 255) / 256), (unsigned)nrows), dim3(256), 0, st>>>(k);
+    LAUNCHCHK();
+    k_odd_irfft<<<dim3((unsigned)((n - 1 + 255) / 256), (unsigned)nrows), dim3(256), 0, st>>>(k, tw, rows, ld);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
 int pss_shift_rows(float *rows, int32_t nrows, int64_t n, int64_t ld, const uint64_t *ramp,
                    const float *nyq, void *work, void *stream) {
+    if (n > 0 && (n & 1) && nrows > 0) {
+        if (n > (1ll << 20)) return fail(PSS_EUNSUPPORTED, "odd-length shift_t above 2^20 samples (N=%lld)", (long long)n);
+        if (ld < n) return fail(PSS_EINVAL, "ld < nsamp");
+        return shift_rows_odd(rows, nrows, n, ld, ramp, work, (hipStream_t)stream);
+    }
     PssPipeline p;
     memset(&p, 0, sizeof(p));
     p.nchan = nrows;
@@ -2523,7 +2728,10 @@ int pss_clip_cast(const float *in, void *out, int64_t count, float clip, int32_t
 
 int pss_fold(const float *data, float *out, int32_t nchan, int64_t ld, int64_t npbins, int64_t n_fold,
              void *stream) {
-    if (nchan <= 0 || npbins < 2) return fail(PSS_EINVAL, "fold geometry");
+    if (nchan <= 0 || npbins < 2 || n_fold < 0) return fail(PSS_EINVAL, "fold geometry");
+    if (npbins + n_fold * (npbins / 2) > ld)
+        return fail(PSS_EINVAL, "fold: %lld + %lld x %lld samples exceed the row (ld %lld)", (long long)npbins,
+                    (long long)n_fold, (long long)(npbins / 2), (long long)ld);
     dim3 g = stream_grid(npbins / 2, nchan);
     hipLaunchKernelGGL(k_fold, g, dim3(256), 0, (hipStream_t)stream, data, out, ld, npbins, n_fold);
     LAUNCHCHK();
@@ -2537,6 +2745,13 @@ int pss_fold_periods(const float *data, float *out, int32_t nchan, int64_t ld, i
                                       (long long)nbin);
     dim3 g = stream_grid(nbin, nchan);
     hipLaunchKernelGGL(k_fold_periods, g, dim3(256), 0, (hipStream_t)stream, data, out, ld, nbin, nper);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+int pss_null_shift(const float *row, int64_t count, int64_t *out, void *stream) {
+    if (!row || !out || count < 1) return fail(PSS_EINVAL, "null_shift: bad arguments");
+    k_null_shift<<<1, 256, 0, (hipStream_t)stream>>>(row, count, out);
     LAUNCHCHK();
     return PSS_OK;
 }

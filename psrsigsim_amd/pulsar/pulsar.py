@@ -4,8 +4,9 @@ make_pulses builds the host plan (Nph, nsamp, nsub, Nfold, draw_norm, the
 spectral-index-scaled PCHIP portrait) exactly as the reference does
 (pulsar.py:86-151) and records a *source* stage; the (Nchan, nsamp)
 intensities -- profile x chi2 draws x draw_norm -- are generated on the GPU
-inside the fused run.  null() derives shift_val / the pulse choice / the
-off-pulse level on the host and records a null stage (pulsar.py:246-333).
+inside the fused run.  null() derives the pulse choice and the off-pulse
+level on the host, shift_val on the device (no host round trip), and records
+a null stage (pulsar.py:246-333).
 """
 import math
 
@@ -192,15 +193,13 @@ class Pulsar(object):
         if pend.null is not None or pend.noise is not None:
             signal._flush()
             pend = _engine.Pending(None)
-        row0 = _engine.probe_row0(signal, pend, Nph)
-        where = np.where(row0 == np.max(row0))[0]
-        shift_val = Nph // 2 - where
+        # shift_val = Nph//2 - argmax(channel 0, first Nph samples), on the
+        # device: no host round trip (a non-unique maximum raises on the
+        # first read of the data, see _engine.check_null_status)
+        shift_dev = _engine.null_shift_device(signal, pend, Nph)
         if length is not None or frequency is not None:
             raise NotImplementedError("Length and Frequency not been implimented yet")
-        if shift_val.size != 1:
-            raise ValueError("operands could not be broadcast together with shapes (%d,) (%d,)"
-                             % (Nph, shift_val.size))
-        shift_val = int(shift_val[0])
+        signal._null_checks = getattr(signal, "_null_checks", []) + [(shift_dev, Nph)]
         call = _engine.next_call()
         rand_pulses = _engine.take_injection("null_pulses")
         if rand_pulses is None:
@@ -211,7 +210,7 @@ class Pulsar(object):
             rank[p] = r
         opm = float(np.mean(self.Profiles._max_profile[opw.astype(int)]))
         dn = float(signal._draw_norm)
-        st = {"rank": rank, "shift_val": shift_val, "nph": Nph, "call_id": call,
+        st = {"rank": rank, "shift_dev": shift_dev, "nph": Nph, "call_id": call,
               "inj_box": _engine.take_injection("box"), "inj_rep": _engine.take_injection("rep")}
         if null_pulses == 0 or rand_pulses.size == 0:
             return

@@ -96,6 +96,7 @@ class FilterBankSignal(BaseSignal):
     @property
     def data(self):
         self._flush()
+        _engine.check_null_status(self)
         return self._buf
 
     def data_numpy(self):

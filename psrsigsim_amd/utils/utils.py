@@ -35,15 +35,14 @@ def shift_t(y, shift, dt=1):
     """utils.py:17-59: delay y by ``shift`` (same units as ``dt``).  Integer
     shift with dt == 1 -> circular roll; otherwise the Fourier shift theorem:
     rfft -> exp(-2 pi i f shift) -> irfft (Nyquist bin keeps cos(pi s)).
-    ``shift`` may be one value per row for a 2-D batch."""
+    For odd N the result has N - 1 samples, as the reference's irfft (no n=)
+    returns.  ``shift`` may be one value per row for a 2-D batch."""
     if isinstance(shift, int) and dt == 1:
         if isinstance(y, torch.Tensor):
             return torch.roll(y, shift, dims=-1)
         return np.roll(y, shift)
     t, was_np, was_1d = _as_rows(y)
     R, N = t.shape
-    if N % 2:
-        raise NotImplementedError("odd-length shift_t (the reference's irfft drops a sample)")
     s = np.broadcast_to(np.asarray(shift, dtype=np.float64) / float(dt), (R,))
     ramp = _engine.u64_to_i64_tensor(_engine.ramp_words(s, N))
     nyq = _engine.to_dev(np.cos(np.pi * s).astype(np.float32))
@@ -51,6 +50,10 @@ def shift_t(y, shift, dt=1):
     rc = _lib.lib().pss_shift_rows(_engine.ptr(t), R, N, t.stride(0), _engine.ptr(ramp),
                                    _engine.ptr(nyq), _engine.ptr(ws), _engine.stream_ptr())
     _lib.check(rc, "shift_t")
+    if N % 2:
+        # odd N: np.fft.irfft without n= returns N - 1 samples (utils.py:57);
+        # the library wrote them into the first N - 1 columns
+        t = t[:, :N - 1]
     return _ret(t, was_np, was_1d)
 
 

@@ -17,4 +17,5 @@ def pytest_configure(config):
 def hip_lib():
     """The built HIP library; on a GPU box a missing library is a failure."""
     from psrsigsim_amd import _lib
+    _lib.check_build_hash()        # the binary under test was built from this tree
     return _lib.lib()

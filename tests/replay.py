@@ -24,6 +24,11 @@ AMBIG = 1e-3   # |shifted null mask - 1| below which the threshold decision is f
 # complex row (direct / Bluestein) have an error relative to the larger of the
 # two (a fold-mode channel peaks at ~5000 against a ~120 mask)
 AMBIG_REL = 1e-5
+# The exclusion may only hide a small, bounded set: at most this fraction of
+# the compared samples may fall in the ambiguity band, and of those at most
+# TOL (as a fraction of all samples) may actually come out on the other side
+# of the threshold (reported as "null_flipped_frac", checked like an error).
+AMBIG_MAX_FRAC = 2e-3
 
 
 def _prof():
@@ -86,8 +91,20 @@ def oracle_exec(case, d):
     sg = case["sig"]
     sig = O.Signal(sg["fcent"], sg["bw"], nchan=sg["nchan"], samprate=sg.get("samprate"),
                    sublen=sg.get("sublen"), dtype=sg.get("dtype", np.float32), fold=sg.get("fold", True))
+    if sg.get("chans") is not None:
+        # only global channels [c0, c1) of the Nchan-channel band (a shard):
+        # their frequencies, and bw/Nchan kept for the radiometer noise
+        c0, c1 = sg["chans"]
+        assert c0 == 0 or not any(op[0] == "null" for op in case["ops"]), \
+            "null's shift_val comes from global channel 0"
+        sig.dat_freq = sig.dat_freq[c0:c1]
+        sig.bw = sig.bw * (c1 - c0) / sig.nchan
+        sig.nchan = c1 - c0
     ps = case["psr"]
-    psr = O.Pulsar(ps["period"], ps["Smean"], profiles=_oracle_profile(ps["prof"]),
+    pspec = ps["prof"]
+    if sg.get("chans") is not None and pspec[0] == "data":
+        pspec = ("data", sig.nchan)     # the same 1-D template on the shard's rows
+    psr = O.Pulsar(ps["period"], ps["Smean"], profiles=_oracle_profile(pspec),
                    specidx=ps.get("specidx", 0.0), ref_freq=ps.get("ref_freq"))
     inj, A = {}, {}
 
@@ -146,6 +163,9 @@ def oracle_run(name):
 # ---------------------------------------------------------------------------
 # product interpretation
 # ---------------------------------------------------------------------------
+_AMB = {"band": 0, "flipped": 0, "total": 0}
+
+
 def _err(gpu, ref, exclude=None, scale_ref=None):
     """Per-channel max|gpu - ref| / max|ref|.  ``scale_ref`` (same shape)
     supplies the magnitude instead: observe's ``out`` is min(data, draw_max)
@@ -156,14 +176,20 @@ def _err(gpu, ref, exclude=None, scale_ref=None):
     ref = np.asarray(ref, dtype=np.float64)
     if gpu.shape != ref.shape:
         return float("inf")
-    if exclude is not None and exclude.shape == ref.shape and exclude.any():
-        gpu = np.where(exclude, ref, gpu)
     ref2 = ref.reshape(ref.shape[0], -1) if ref.ndim > 1 else ref[None]
-    gpu2 = gpu.reshape(ref2.shape)
     mag = ref2
     if scale_ref is not None and np.shape(scale_ref) == ref.shape:
         mag = np.maximum(np.abs(ref2), np.abs(np.asarray(scale_ref, dtype=np.float64).reshape(ref2.shape)))
     scale = np.maximum(np.max(np.abs(mag), axis=1), 1e-30)
+    if exclude is not None and exclude.shape == ref.shape and exclude.any():
+        # count what the exclusion hides: samples in the band, and those whose
+        # null decision actually differs from the reference's
+        off = np.abs(gpu.reshape(ref2.shape) - ref2) > 1e-5 * scale[:, None]
+        _AMB["band"] += int(exclude.sum())
+        _AMB["flipped"] += int((exclude.reshape(ref2.shape) & off).sum())
+        _AMB["total"] += int(ref.size)
+        gpu = np.where(exclude, ref, gpu)
+    gpu2 = gpu.reshape(ref2.shape)
     return float(np.max(np.max(np.abs(gpu2 - ref2), axis=1) / scale))
 
 
@@ -171,6 +197,7 @@ def run_case(name, fused=True, case=None, seed=None):
     """Replay a golden case (``name``) -- or, with ``case``/``seed``, any case
     script against the oracle run with legacy RandomState(seed) draws."""
     import psrsigsim_amd as pss
+    import psrsigsim_amd._engine  # noqa: F401
     from psrsigsim_amd.signal import FilterBankSignal
     from psrsigsim_amd.pulsar import Pulsar, GaussProfile, DataProfile
     from psrsigsim_amd.ism import ISM
@@ -184,9 +211,16 @@ def run_case(name, fused=True, case=None, seed=None):
     else:
         A, inj = oracle_exec(case, O.LegacyDraws(seed))
     sg = case["sig"]
+    chans = sg.get("chans")
     sig = FilterBankSignal(sg["fcent"], sg["bw"], Nsubband=sg["nchan"], sample_rate=sg.get("samprate"),
                            sublen=sg.get("sublen"), dtype=sg.get("dtype", np.float32),
-                           fold=sg.get("fold", True))
+                           fold=sg.get("fold", True), shard=chans)
+
+    def rows(a):
+        # a shard's injected draws: the oracle computed only its channels
+        return pss._engine.RowBlock(chans[0], a) if (chans is not None and a is not None) else a
+    for _AMB_k in _AMB:
+        _AMB[_AMB_k] = 0
     ps = case["psr"]
     spec = ps["prof"]
     if spec[0] == "gauss":
@@ -214,7 +248,7 @@ def run_case(name, fused=True, case=None, seed=None):
     for op in case["ops"]:
         k = op[0]
         if k == "make_pulses":
-            pss.inject(gen=inj["gen"])
+            pss.inject(gen=rows(inj["gen"]))
             psr.make_pulses(sig, op[1])
             snap(op[2])
         elif k == "disperse":
@@ -231,7 +265,7 @@ def run_case(name, fused=True, case=None, seed=None):
         elif k == "null":
             pss.inject(null_pulses=inj["null_pulses"], box=inj["box"])
             if inj["rep"] is not None:
-                pss.inject(rep=inj["rep"])
+                pss.inject(rep=rows(inj["rep"]))
             psr.null(sig, op[1])
             amb["mask"] = inj.get("ambiguous")
             snap(op[2])
@@ -246,7 +280,7 @@ def run_case(name, fused=True, case=None, seed=None):
                 tel.add_system(name="T", receiver=Receiver(fcent=1400, bandwidth=400, name="Lband"),
                                backend=Backend(samprate=1.0 / Quantity(tel_spec[1], "s"), name="Cyborg"))
             if noise:
-                pss.inject(noise=inj["noise"])
+                pss.inject(noise=rows(inj["noise"]))
             pre = A.get("data_" + seen[-1]) if seen else None
             out = tel.observe(sig, psr, system=system, noise=noise, ret_resampsig=True)
             errs["out"] = _err(out.cpu().numpy().astype(np.float64), A["out"], amb["mask"], scale_ref=pre)
@@ -256,4 +290,12 @@ def run_case(name, fused=True, case=None, seed=None):
     last = [op for op in case["ops"] if op[-1] is not None and op[0] != "observe"]
     if fused and case["ops"][-1][0] != "observe" and last:
         errs[last[-1][-1]] = _err(sig.data.cpu().numpy(), A["data_" + last[-1][-1]], amb["mask"])
+    if _AMB["total"]:
+        band = _AMB["band"] / _AMB["total"]
+        assert band <= AMBIG_MAX_FRAC, "null threshold ambiguity band holds %.3g of the samples" % band
+        errs["null_flipped_frac"] = _AMB["flipped"] / _AMB["total"]
+        STATS["ambiguous_band_frac"] = band
     return errs
+
+
+STATS = {}

@@ -30,6 +30,17 @@ def test_library_loads_and_exports_everything():
     assert L.pss_version() >= 100
 
 
+def test_library_built_from_these_sources():
+    """The binary that tests and benchmarks load is the one built from HEAD's
+    sources: its embedded sha256 equals the hash of the sources in the tree
+    (psrsigsim_amd/build.py; content, not mtimes)."""
+    from psrsigsim_amd import build
+    L = _lib.load()
+    assert L.pss_build_hash().decode() == "PSS_BUILD_HASH=" + build.source_hash()
+    assert build.embedded_hash() == build.source_hash()
+    assert not build.stale()
+
+
 def test_workspace_sizes():
     L = _lib.load()
     # [spill area, 256-B aligned regions][null mask row: nsamp floats]
@@ -86,3 +97,14 @@ def test_error_mapping():
         _lib.check(_lib.PSS_EUNSUPPORTED)
     with pytest.raises(RuntimeError):
         _lib.check(_lib.PSS_EHIP)
+
+
+def test_fold_rejects_out_of_row_geometry():
+    """pss_fold validates its geometry at the C ABI (no GPU touched): the
+    npbins + n_fold * npbins/2 samples it sums must lie inside the row."""
+    L = _lib.load()
+    assert L.pss_fold(None, None, 2, 100, 64, 3, None) == _lib.PSS_EINVAL     # 64 + 3*32 > 100
+    assert L.pss_fold(None, None, 2, 100, 1, 3, None) == _lib.PSS_EINVAL      # npbins < 2
+    assert L.pss_fold(None, None, 0, 100, 64, 1, None) == _lib.PSS_EINVAL     # no rows
+    L.pss_fold(None, None, 2, 100, 64, 3, None)
+    assert "exceed the row" in _lib.last_error()

@@ -65,9 +65,11 @@ def test_shard_invariance_bitwise(log2n, hip_lib):
     np.testing.assert_array_equal(np.vstack([a, b]), full)
 
 
-@pytest.mark.parametrize("nchan,log2n,null", [(3, 16, True), (4, 17, True), (5, 14, True), (2, 16, False),
-                                             (3, 22, True)])
-def test_fast_path_bitwise_equals_generic(nchan, log2n, null, hip_lib):
+@pytest.mark.parametrize("nchan,log2n,null,dm", [(3, 16, True, 100), (4, 17, True, 100), (5, 14, True, 100),
+                                                (2, 16, False, 100), (3, 22, True, 100),
+                                                # C5's per-GPU geometry: 2^24 (2048 x 8192 split), DM 500
+                                                (2, 24, True, 500)])
+def test_fast_path_bitwise_equals_generic(nchan, log2n, null, dm, hip_lib):
     """The fast-path kernels (Philox df=1, no injection: the north-star
     configuration) against the generic kernels, bit for bit."""
     from psrsigsim_amd import _lib
@@ -82,7 +84,7 @@ def test_fast_path_bitwise_equals_generic(nchan, log2n, null, hip_lib):
         sig = FilterBankSignal(1400, 400, Nsubband=nchan, fold=False)
         psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
         psr.make_pulses(sig, tobs=(1 << log2n) * 20.48e-6)
-        ISM().disperse(sig, 100)
+        ISM().disperse(sig, dm)
         if null:
             psr.null(sig, 0.2)
         T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True)

@@ -132,3 +132,27 @@ def test_gather_channels_gloo(world, nchan):
         p.join(120)
         assert p.exitcode == 0
     assert q.get(timeout=10) == 1
+
+
+def test_bench_self_launch_world2():
+    """bench.py --gpus 2 started directly launches its two ranks itself
+    (torch.distributed.run child process, 127.0.0.1) and rank 0 prints one
+    JSON line reporting both ranks -- here in --dry-run (gloo, host planning
+    only), the same launcher path the GPU run takes with RCCL."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for scaling in ("weak", "strong"):
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1",
+                            "--warmup", "0", "--dry-run", "--log2n", "14", "--nchan", "8", "--scaling", scaling],
+                           capture_output=True, text=True, timeout=300, cwd=root)
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+        assert len(lines) == 1, r.stdout
+        line = json.loads(lines[0])
+        assert line["n_gpus"] == 2 and line["ranks"] == 2
+        assert line["scaling"] == scaling
+        assert line["config"]["nchan_total"] == (16 if scaling == "weak" else 8)
+        assert line["config"]["nchan_per_gpu"] == (8 if scaling == "weak" else 4)
+        assert line["value"] > 0

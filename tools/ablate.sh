@@ -31,7 +31,9 @@ for v in base $VARIANTS; do
   lib=$R/psrsigsim_amd/libpss_hip_abl$t.so
   [ "$v" = base ] && lib=$R/psrsigsim_amd/libpss_hip.so
   echo "== variant $v"
-  PSS_LIB_PATH=$lib timeout -k 10 300 python $R/tools/kernel_lab.py --no-fill --reps 2 ${LAB_VARIANTS:-full nonull_nonoise} \
-      > $OUT/${TAG}_$t.log 2>&1 || { echo "variant $v failed"; tail -5 $OUT/${TAG}_$t.log; exit 1; }
-  grep -v negative $OUT/${TAG}_$t.log | grep wall
+  for fl in ${LAB_FLAGS:-0}; do
+  PSS_LIB_PATH=$lib timeout -k 10 300 python $R/tools/kernel_lab.py --no-fill --reps 2 --flags $fl ${LAB_VARIANTS:-full nonull_nonoise} \
+      > $OUT/${TAG}_${t}_f$fl.log 2>&1 || { echo "variant $v failed"; tail -5 $OUT/${TAG}_${t}_f$fl.log; exit 1; }
+  echo "flags $fl"; grep -v negative $OUT/${TAG}_${t}_f$fl.log | grep wall
+  done
 done

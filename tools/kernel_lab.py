@@ -38,12 +38,14 @@ def main():
     ap.add_argument("--log2n", type=int, default=22)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--no-fill", action="store_true")
+    ap.add_argument("--flags", type=int, default=0, help="pss_set_flags value (e.g. 4 = no pipelined kernels)")
     ap.add_argument("variants", nargs="*", default=["full", "nonoise", "nonull", "nonull_nonoise"])
     a = ap.parse_args()
     import torch
     import psrsigsim_amd as pss
     from psrsigsim_amd import _lib
     L = _lib.lib()
+    L.pss_set_flags(a.flags)
     pss.seed(1)
     res = {}
     for v in a.variants:

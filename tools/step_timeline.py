@@ -15,16 +15,16 @@ def main():
     from psrsigsim_amd.telescope import telescope as T
     nchan = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
     pss.seed(1)
-    orig = _engine.probe_row0
+    orig = _engine.null_shift_device
 
     def probe(*a, **k):
         t = time.perf_counter()
         r = orig(*a, **k)
         print("    probe %.2f ms" % ((time.perf_counter() - t) * 1e3))
         return r
-    _engine.probe_row0 = probe
+    _engine.null_shift_device = probe
     import psrsigsim_amd.pulsar.pulsar as PP
-    PP._engine.probe_row0 = probe
+    PP._engine.null_shift_device = probe
     ms = torch.cuda.Stream() if os.environ.get("MAIN_STREAM") else None
     if ms is not None:
         torch.cuda.set_stream(ms)
