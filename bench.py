@@ -78,21 +78,34 @@ def c3_step(pss, nchan_total, shard, nsamp_log2, ret_out=False):
 
 
 F0_B1855 = 186.4940812499314404
+_B1855 = {}
+
+
+def b1855_profile():
+    """Config C4's template profile (read once per process)."""
+    if "p" not in _B1855:
+        from psrsigsim_amd.io.psrfits import template_profile
+        from psrsigsim_amd.data import B1855_TEMPLATE
+        _B1855["p"] = template_profile(B1855_TEMPLATE)
+    return _B1855["p"]
 
 
 def c4_step(pss, nchan_total, shard, gather):
     """BASELINE config C4: fold mode, 30 subints x 1024 bins over 30 min
     (30720 samples per channel: the mixed-radix 30 x 1024 four-step), DM 13.3,
     Arecibo radiometer noise; the folded filterbank is gathered to rank 0 over
-    RCCL (psrsigsim_amd.shard) inside the step.  Gaussian portrait (the
-    B1855+09 template file is not read at run time)."""
+    RCCL (psrsigsim_amd.shard) inside the step.  Portrait: the B1855+09
+    template's profile (DATA * DAT_SCL + DAT_OFFS of the reference's
+    data/B1855+09.L-wide.PUPPI.11y.x.sum.sm, median baseline removed; read once
+    by the FITS reader, outside the timed region) as a DataProfile tiled over
+    the channels."""
     from psrsigsim_amd.signal import FilterBankSignal
-    from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+    from psrsigsim_amd.pulsar import Pulsar, DataProfile
     from psrsigsim_amd.ism import ISM
     from psrsigsim_amd.telescope import telescope as T
     sig = FilterBankSignal(1400, 400, Nsubband=nchan_total, sample_rate=F0_B1855 * 1024 * 1e-6, sublen=60.0,
                            fold=True, shard=shard)
-    psr = Pulsar(1.0 / F0_B1855, 0.005, profiles=GaussProfile(0.5, 0.05, 1))
+    psr = Pulsar(1.0 / F0_B1855, 0.005, profiles=DataProfile(b1855_profile(), Nchan=nchan_total))
     psr.make_pulses(sig, tobs=1800.0)
     ISM().disperse(sig, 13.299393)
     T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True)
@@ -140,8 +153,8 @@ WORKLOADS = {
           "disperse(DM=15.917131) + GBT Lband_GUPPI radiometer noise",
     "c3": "C3 north-star: FilterBankSignal 2048 ch x 2^22 samp per GPU, GaussProfile P=5 ms, "
           "scatter_broaden(1e-4 s, convolve) + disperse(DM=100) + null(0.1) + Arecibo Lband_PUPPI radiometer noise",
-    "c4": "C4: fold mode 2048 ch x (30 subints x 1024 bins) per GPU, P=1/186.49 Hz, disperse(DM=13.3) + "
-          "Arecibo noise, RCCL gather of the folded filterbank to rank 0",
+    "c4": "C4: fold mode 2048 ch x (30 subints x 1024 bins) per GPU, P=1/186.49 Hz, B1855+09 template "
+          "DataProfile, disperse(DM=13.3) + Arecibo noise, RCCL gather of the folded filterbank to rank 0",
     "c5": "C5 per GPU: 1024 ch x 2^24 samp (8192 ch over 8 GPUs), GaussProfile P=5 ms, disperse(DM=500) + "
           "Arecibo noise",
 }

@@ -183,6 +183,10 @@ int pss_last_error(char *buf, size_t n);
  * processed; returns the number of launches reported and resets. */
 void pss_timing_enable(int on);
 int pss_timing_collect(int32_t *kind, double *ms, int64_t *units, int cap);
+/* Milliseconds from the start of the first timed launch to the end of the
+ * last one since the last collect (the device span of the runs: with pair
+ * batches on side streams the per-kernel times overlap). */
+double pss_timing_span_ms(void);
 
 /* Workspace bytes the fused run needs for `nchan` rows of length `nsamp`. */
 int64_t pss_workspace_bytes(int32_t nchan, int64_t nsamp);

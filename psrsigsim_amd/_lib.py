@@ -53,6 +53,7 @@ EXPORTS = {
     "pss_last_error": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
     "pss_workspace_bytes": (c_i64, [c_i32, c_i64]),
     "pss_timing_enable": (None, [ctypes.c_int]),
+    "pss_timing_span_ms": (ctypes.c_double, []),
     "pss_timing_collect": (ctypes.c_int, [ctypes.POINTER(c_i32), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(c_i64), ctypes.c_int]),
     "pss_run": (ctypes.c_int, [ctypes.POINTER(PssPipeline), c_vp]),

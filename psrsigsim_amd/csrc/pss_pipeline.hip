@@ -41,6 +41,11 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 #define PSS_BC 16
 #define PSS_TC 1024
 #endif
+// pass A: PCHIP interval / fraction of consecutive samples by increments
+// (PhaseWalk) instead of per-sample multiplies (experiment switch)
+#ifndef PSS_PHASE_WALK
+#define PSS_PHASE_WALK 1
+#endif
 // cache policy bits of the column passes' spill loads (experiment switch;
 // gfx950 buffer aux: 1 = sc0, 2 = nt, 16 = sc1)
 #ifndef PSS_SPILL_AUX
@@ -135,6 +140,7 @@ struct KP {
     const uint32_t *mbits;  // [nchan][N/32] per-channel null decisions (k_mask_bits)
     int mbB;                // column-block width B of pass C (mbits layout)
     const cf *rtab;         // [nchan][RFL] row-pass ramp factors (k_ramp_tab)
+    hipEvent_t after_a;     // batching: recorded after this launch's pass A (or NULL)
 };
 
 // ---------------------------------------------------------------------------
@@ -1132,7 +1138,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
     // A: generate channels a, b into z = d_a + i d_b; column FFTs; twiddle; spill.
     // FAST (host-selected): search-mode source with Philox chi2(1) draws, no
     // injected draws, no undelayed null -- the same values as source4.
-    template <bool FAST>
+    template <bool FAST, bool SHARED = false>
     __device__ static void passA(const KP &k) {
         __shared__ cf lds[B * Lds<N1>::RS];
         const int tid = threadIdx.x;
@@ -1156,22 +1162,22 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
             const int nint = p.nint;
             const int last = p.prof_rows - 1;
             const int rowa = min(max(pra, 0), last), rowb = min(max(prb, 0), last);
-#ifdef PSS_OLD_PA   // A/B switch (tools/ablate.sh): two table rows, per-sample phase multiplies
-            const bool shared = false;
-#else
-            const bool shared = rowa == rowb;            // one table row for both (e.g. C3's GaussProfile)
-#endif
+            // SHARED (host-selected: prof_rows == 1, e.g. C3's GaussProfile):
+            // one table row serves both channels, one lookup and evaluation
+            constexpr bool shared = SHARED;
             const float4 *prof = reinterpret_cast<const float4 *>(p.prof);
             for (int i = tid; i < nint; i += T) {
                 ptab[0][i] = prof[(int64_t)rowa * nint + i];
-                if (!shared) ptab[1][i] = prof[(int64_t)rowb * nint + i];
+                if constexpr (!shared) ptab[1][i] = prof[(int64_t)rowb * nint + i];
             }
             __syncthreads();
             const float dn = p.draw_norm;
+#if PSS_PHASE_WALK
             uint32_t dlo;
             uint64_t dhi;
             phase_delta(p, dlo, dhi);
             const uint32_t M = p.knot_m;
+#endif
 #pragma unroll
             for (int t = 0; t < ITEMS; ++t) {
                 const int it = tid + t * T;
@@ -1181,22 +1187,24 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
                 const float4 qa = chi2_1x4(g.bits(n >> 2, ca, 0u));
                 const float4 qb = chi2_1x4(g.bits(n >> 2, cb, 0u));
                 const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
+#if PSS_PHASE_WALK
                 PhaseWalk w;
                 w.start(p, n);
+#endif
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     uint32_t iv;
                     float u;
-#ifdef PSS_OLD_PA
-                    pchip_locate(k, (int64_t)(n + (uint32_t)i), iv, u);
-#else
+#if PSS_PHASE_WALK
                     if (i) w.step(dlo, dhi, M);
                     w.get(p, iv, u);
+#else
+                    pchip_locate(k, (int64_t)(n + (uint32_t)i), iv, u);
 #endif
                     const float4 A = ptab[0][iv];
                     const float pa = fmaf(fmaf(fmaf(A.x, u, A.y), u, A.z), u, A.w);
                     float pb = pa;
-                    if (!shared) {
+                    if constexpr (!shared) {
                         const float4 Bc = ptab[1][iv];
                         pb = fmaf(fmaf(fmaf(Bc.x, u, Bc.y), u, Bc.z), u, Bc.w);
                     }
@@ -1447,8 +1455,8 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
 
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairA(KP k) { C::template passA<false>(k); }
-template <typename C, int T>
-__global__ __launch_bounds__(T) void k_pairA_fast(KP k) { C::template passA<true>(k); }
+template <typename C, int T, bool SHARED>
+__global__ __launch_bounds__(T) void k_pairA_fast(KP k) { C::template passA<true, SHARED>(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairC(KP k) { C::passC(k); }
 template <typename C, int T>
@@ -2201,6 +2209,87 @@ static int build_mask_table(KP &k, hipStream_t st, const float *mask_row, char *
     return PSS_OK;
 }
 
+// Pair batches on two side streams (PSS_BATCHES > 1, fast path only): batch
+// b's pass A waits for batch b-1's pass A, so it runs next to batch b-1's
+// row pass (82 + 70 KB of LDS: both fit one CU) -- the compute-heavy
+// generator overlaps the memory-heavy passes instead of the three passes
+// running one after the other over all channels.  The batches are
+// independent pair ranges (per-row arrays offset, RNG keyed by global
+// channel): results are bitwise those of one launch.  Fork from / join to
+// the caller's stream with events, so the run stays stream-ordered.
+static int g_batches = -1;
+static int batches_setting() {
+    if (g_batches < 0) {
+        const char *e = getenv("PSS_BATCHES");
+        g_batches = e ? atoi(e) : 1;
+        if (g_batches < 1) g_batches = 1;
+        if (g_batches > 16) g_batches = 16;
+    }
+    return g_batches;
+}
+struct SideStreams {
+    hipStream_t s[2];
+    hipEvent_t ev[40];
+    bool ok;
+};
+static SideStreams *side_streams() {
+    static SideStreams g[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    SideStreams &x = g[dev];
+    if (!x.ok) {
+        for (int i = 0; i < 2; ++i)
+            if (hipStreamCreateWithFlags(&x.s[i], hipStreamNonBlocking) != hipSuccess) return nullptr;
+        for (int i = 0; i < 40; ++i)
+            if (hipEventCreateWithFlags(&x.ev[i], hipEventDisableTiming) != hipSuccess) return nullptr;
+        x.ok = true;
+    }
+    return &x;
+}
+
+template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typename RF, typename RI,
+          int TRF, int BC, int TC>
+static int launch_pair_passes(KP &k, hipStream_t st);
+
+template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typename RF, typename RI,
+          int TRF, int BC, int TC>
+static int launch_batches(KP &k, hipStream_t st, int nb) {
+    using PR = PairRows<N2, TR, RF, RI>;
+    SideStreams *ss = side_streams();
+    if (!ss) return fail(PSS_EHIP, "side streams");
+    hipEvent_t fork = ss->ev[0];
+    HIPCHK(hipEventRecord(fork, st));
+    for (int i = 0; i < 2; ++i) HIPCHK(hipStreamWaitEvent(ss->s[i], fork, 0));
+    for (int b = 0; b < nb; ++b) {
+        const int p0 = (int)((int64_t)b * k.npairs / nb), p1 = (int)((int64_t)(b + 1) * k.npairs / nb);
+        const int r0 = p0 == 0 ? 0 : 2 * p0 - k.poff;
+        const int r1 = min(2 * p1 - k.poff, k.p.nchan);
+        KP kb = k;
+        kb.poff = p0 == 0 ? k.poff : 0;
+        kb.npairs = p1 - p0;
+        kb.p.nchan = r1 - r0;
+        kb.p.chan0 = k.p.chan0 + r0;
+        kb.p.data = k.p.data + (int64_t)r0 * k.p.ld;
+        kb.p.ramp = k.p.ramp + r0;
+        kb.p.nyq_re = k.p.nyq_re + r0;
+        kb.p.nyq_im = k.p.nyq_im + r0;
+        if (k.p.mask_ramp) kb.p.mask_ramp = k.p.mask_ramp + r0;
+        kb.rtab = k.rtab + (int64_t)r0 * PR::RFL;
+        kb.Yd = k.Yd + (int64_t)p0 * k.N;
+        kb.after_a = ss->ev[1 + b];
+        hipStream_t sb = ss->s[b & 1];
+        if (b > 0) HIPCHK(hipStreamWaitEvent(sb, ss->ev[b], 0));     // batch b-1's pass A done
+        const int rc = launch_pair_passes<N1, B, T, CF, CI, N2, TR, RF, RI, TRF, BC, TC>(kb, sb);
+        if (rc) return rc;
+    }
+    for (int i = 0; i < 2; ++i) {
+        hipEvent_t j = ss->ev[20 + i];
+        HIPCHK(hipEventRecord(j, ss->s[i]));
+        HIPCHK(hipStreamWaitEvent(st, j, 0));
+    }
+    return PSS_OK;
+}
+
 // BC/TC: column-block width and threads of the FAST pass C (the spill layout
 // does not depend on the block width, so pass C may use wider blocks than pass
 // A: its output rows are written in BC-sample (4 BC-byte) segments).
@@ -2240,16 +2329,34 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
         LAUNCHCHK();
         k.rtab = rt;
     }
+    const bool fast = PCC::kItemsExact && fast_epilogue(k);
+    const int nb = (fast && fast_source(k.p) && g_batches > 1 && k.npairs >= 4 * g_batches) ? g_batches : 1;
+    if (nb > 1) return launch_batches<N1, B, T, CF, CI, N2, TR, RF, RI, TRF, BC, TC>(k, st, nb);
+    return launch_pair_passes<N1, B, T, CF, CI, N2, TR, RF, RI, TRF, BC, TC>(k, st);
+}
+
+// The passes of one pair range (after the mask table and the ramp table).
+template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typename RF, typename RI,
+          int TRF, int BC, int TC>
+static int launch_pair_passes(KP &k, hipStream_t st) {
+    using PC = PairCols<N1, B, T, CF, CI>;
+    using PCC = PairCols<N1, BC, TC, CF, CI>;
+    using PR = PairRows<N2, TR, RF, RI>;
     dim3 gc((unsigned)(N2 / B), (unsigned)k.npairs);
     tk_begin(TK_COLA, st);
     if constexpr (PC::kItemsExact) {
-        if (fast_source(k.p)) k_pairA_fast<PC, T><<<gc, dim3(T), 0, st>>>(k);
-        else k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
+        if (fast_source(k.p)) {
+            if (k.p.prof_rows == 1) k_pairA_fast<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
+            else k_pairA_fast<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
+        } else {
+            k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
+        }
     } else {
         k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
     }
     tk_end(st);
     LAUNCHCHK();
+    if (k.after_a) HIPCHK(hipEventRecord(k.after_a, st));   // batching: the next batch's pass A may start
     tk_begin(TK_ROW, st);
     k_pair_row<PR, TR><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
     tk_end(st);
@@ -2548,6 +2655,14 @@ void pss_timing_enable(int on) {
     g_timing = on != 0;
 }
 
+double pss_timing_span_ms(void) {
+    if (g_ntl < 1) return 0.0;
+    float e = 0.f;
+    (void)hipEventSynchronize(g_tl[g_ntl - 1].b);
+    if (hipEventElapsedTime(&e, g_tl[0].a, g_tl[g_ntl - 1].b) != hipSuccess) return -1.0;
+    return e;
+}
+
 int pss_timing_collect(int32_t *kind, double *ms, int64_t *units, int cap) {
     int n = 0;
     for (int i = 0; i < g_ntl; ++i) {
@@ -2579,6 +2694,7 @@ int64_t pss_workspace_bytes(int32_t nchan, int64_t nsamp) {
 int pss_run(const PssPipeline *p, void *stream) {
     int rc = validate(p);
     if (rc) return rc;
+    batches_setting();
     hipStream_t st = (hipStream_t)stream;
     KP k;
     memset(&k, 0, sizeof(k));

@@ -15,8 +15,15 @@ producing the same data layout without a template:
   truncated to '>i2' (psrfits.py:355-366); header NBIN, NCHAN, NPOL = 1,
   TBIN = P / nbin, CHAN_BW, DM, POL_TYPE = 'AA+BB', EPOCHS = 'MIDTIME'.
 
+The SUBINT column set, order, TFORM codes and TDIM follow the reference's
+template (``data/B1855+09.L-wide.PUPPI.11y.x.sum.sm``, whose SUBINT table the
+reference copies, psrfits.py:487-509): the pointing/angle columns the
+reference leaves at their draft value are written as zeros.
+
 No POLYCO / PSRPARAM tables (PINT is absent): files are not phase-connected.
-``read_psrfits`` parses what ``save`` writes (tests, and round trips).
+``read_fits`` parses any FITS file of binary tables (the reference's
+template included, for config C4's portrait: :func:`template_profile`);
+``read_psrfits`` returns the primary and SUBINT parts of it.
 The device data is read back once (one D2H copy of the folded product; in a
 multi-GPU run gather it first with ``psrsigsim_amd.shard.gather_channels``).
 """
@@ -26,7 +33,14 @@ import numpy as np
 
 from .._units import Quantity
 
-__all__ = ["PSRFITS", "read_psrfits"]
+__all__ = ["PSRFITS", "read_psrfits", "read_fits", "template_profile"]
+
+# SUBINT columns of the reference's template, in its order (the pointing /
+# angle columns carry zeros here: no telescope geometry is simulated)
+_SUBINT_SCALARS = [("INDEXVAL", "D"), ("TSUBINT", "D"), ("OFFS_SUB", "D"), ("LST_SUB", "D"), ("RA_SUB", "D"),
+                   ("DEC_SUB", "D"), ("GLON_SUB", "D"), ("GLAT_SUB", "D"), ("FD_ANG", "E"), ("POS_ANG", "E"),
+                   ("PAR_ANG", "E"), ("TEL_AZ", "E"), ("TEL_ZEN", "E"), ("AUX_DM", "D"), ("AUX_RM", "D")]
+_NP = {"D": ">f8", "E": ">f4", "I": ">i2", "J": ">i4", "K": ">i8", "B": "u1", "L": "u1", "A": "S1"}
 
 _BLOCK = 2880
 
@@ -121,14 +135,16 @@ class PSRFITS(object):
             _card("OBSNCHAN", nchan), _card("CHAN_DM", dm), _card("STT_IMJD", imjd), _card("STT_SMJD", smjd),
             _card("STT_OFFS", offs), _card("BE_DELAY", 0.0),
         ]
-        cols = [("TSUBINT", "1D", None), ("OFFS_SUB", "1D", None), ("DAT_FREQ", "%dD" % nchan, None),
-                ("DAT_WTS", "%dE" % nchan, None), ("DAT_OFFS", "%dE" % (nchan * npol), None),
-                ("DAT_SCL", "%dE" % (nchan * npol), None),
-                ("DATA", "%dI" % (nbin * nchan * npol), "(%d,%d,%d)" % (nbin, nchan, npol))]
-        row = np.dtype([("TSUBINT", ">f8"), ("OFFS_SUB", ">f8"), ("DAT_FREQ", ">f8", (nchan,)),
-                        ("DAT_WTS", ">f4", (nchan,)), ("DAT_OFFS", ">f4", (nchan * npol,)),
-                        ("DAT_SCL", ">f4", (nchan * npol,)), ("DATA", ">i2", (npol, nchan, nbin))])
+        cols = [(n, "1" + c, None) for n, c in _SUBINT_SCALARS]
+        cols += [("DAT_FREQ", "%dD" % nchan, None), ("DAT_WTS", "%dE" % nchan, None),
+                 ("DAT_OFFS", "%dE" % (nchan * npol), None), ("DAT_SCL", "%dE" % (nchan * npol), None),
+                 ("DATA", "%dI" % (nbin * nchan * npol), "(%d,%d,%d)" % (nbin, nchan, npol))]
+        row = np.dtype([(n, _NP[c]) for n, c in _SUBINT_SCALARS] +
+                       [("DAT_FREQ", ">f8", (nchan,)), ("DAT_WTS", ">f4", (nchan,)),
+                        ("DAT_OFFS", ">f4", (nchan * npol,)), ("DAT_SCL", ">f4", (nchan * npol,)),
+                        ("DATA", ">i2", (npol, nchan, nbin))])
         tab = np.zeros(nsub, dtype=row)
+        tab["INDEXVAL"] = np.arange(nsub)
         tab["TSUBINT"] = sublen
         tab["OFFS_SUB"] = sublen / 2.0 + np.arange(nsub) * sublen
         tab["DAT_FREQ"] = freqs
@@ -158,49 +174,127 @@ class PSRFITS(object):
 
 
 def _parse_header(buf, pos):
+    """(cards dict, position after the header) of the header at ``pos``."""
     cards = {}
-    order = []
     while True:
-        block = buf[pos:pos + _BLOCK].decode("ascii")
+        block = buf[pos:pos + _BLOCK].decode("ascii", errors="replace")
+        if len(block) < _BLOCK:
+            raise ValueError("truncated FITS header")
         pos += _BLOCK
-        done = False
         for i in range(0, _BLOCK, 80):
             c = block[i:i + 80]
             key = c[:8].strip()
             if key == "END":
-                done = True
-                break
+                return cards, pos
             if c[8:10] == "= ":
-                v = c[10:].split(" / ")[0].strip()
-                if v.startswith("'"):
-                    v = v[1:v.rindex("'")].rstrip().replace("''", "'")
-                elif v in ("T", "F"):
-                    v = v == "T"
+                v = c[10:]
+                if v.lstrip().startswith("'"):
+                    v = v.lstrip()
+                    j = 1
+                    out = []
+                    while j < len(v):            # quoted string, '' escapes a quote
+                        if v[j] == "'":
+                            if j + 1 < len(v) and v[j + 1] == "'":
+                                out.append("'")
+                                j += 2
+                                continue
+                            break
+                        out.append(v[j])
+                        j += 1
+                    v = "".join(out).rstrip()
                 else:
-                    v = float(v) if any(ch in v for ch in ".EeDd") else int(v)
+                    v = v.split("/")[0].strip()
+                    if v in ("T", "F"):
+                        v = v == "T"
+                    elif v == "":
+                        v = None
+                    else:
+                        try:
+                            v = int(v)
+                        except ValueError:
+                            v = float(v.replace("D", "E"))
                 cards[key] = v
-                order.append(key)
-        if done:
-            return cards, pos
+
+
+def _table_dtype(hdr):
+    """numpy dtype of a BINTABLE row (TFORM rTa codes D E I J K B L A; TDIM
+    reshapes, fastest axis first as FITS writes them)."""
+    fields = []
+    for i in range(1, int(hdr["TFIELDS"]) + 1):
+        form = str(hdr["TFORM%d" % i]).strip()
+        k = 0
+        while k < len(form) and form[k].isdigit():
+            k += 1
+        n, code = int(form[:k] or 1), form[k]
+        if code not in _NP:
+            raise NotImplementedError("FITS column format %r" % form)
+        shape = (n,) if n > 1 else ()
+        dim = hdr.get("TDIM%d" % i)
+        if dim and n > 1:
+            shape = tuple(int(x) for x in str(dim).strip("() ").split(","))[::-1]
+        if code == "A":
+            fields.append((hdr["TTYPE%d" % i], "S%d" % n))
+        else:
+            fields.append((hdr["TTYPE%d" % i], _NP[code], shape))
+    dt = np.dtype(fields)
+    if dt.itemsize != int(hdr["NAXIS1"]):
+        raise ValueError("row layout %d B != NAXIS1 %d" % (dt.itemsize, hdr["NAXIS1"]))
+    return dt
+
+
+def read_fits(path):
+    """All HDUs of a FITS file of binary tables (PSRFITS):
+    ``{"PRIMARY": (header, None), EXTNAME: (header, records or None)}``."""
+    with open(path, "rb") as f:
+        buf = f.read()
+    out = {}
+    pos = 0
+    while pos < len(buf):
+        hdr, pos = _parse_header(buf, pos)
+        if "SIMPLE" in hdr:
+            name, size = "PRIMARY", 0
+            if int(hdr.get("NAXIS", 0)) > 0:
+                size = abs(int(hdr["BITPIX"])) // 8
+                for a in range(1, int(hdr["NAXIS"]) + 1):
+                    size *= int(hdr["NAXIS%d" % a])
+            out[name] = (hdr, None)
+        else:
+            name = str(hdr.get("EXTNAME", "HDU%d" % len(out))).strip()
+            size = int(hdr["NAXIS1"]) * int(hdr["NAXIS2"]) + int(hdr.get("PCOUNT", 0))
+            rec = None
+            if hdr.get("XTENSION") == "BINTABLE":
+                try:
+                    rec = np.frombuffer(buf, dtype=_table_dtype(hdr), count=int(hdr["NAXIS2"]), offset=pos)
+                except NotImplementedError:
+                    rec = None
+            out[name] = (hdr, rec)
+        pos += -(-size // _BLOCK) * _BLOCK
+    return out
 
 
 def read_psrfits(path):
-    """(primary header dict, SUBINT header dict, SUBINT records) of a file
-    written by :meth:`PSRFITS.save`."""
-    buf = open(path, "rb").read()
-    prim, pos = _parse_header(buf, 0)
-    sub, pos = _parse_header(buf, pos)
-    fmt = {"D": ">f8", "E": ">f4", "I": ">i2", "J": ">i4"}
-    fields = []
-    for i in range(1, sub["TFIELDS"] + 1):
-        form = sub["TFORM%d" % i]
-        n, code = int(form[:-1] or 1), form[-1]
-        shape = (n,) if n > 1 else ()
-        dim = sub.get("TDIM%d" % i)
-        if dim:
-            shape = tuple(int(x) for x in dim.strip("()").split(","))[::-1]
-        fields.append((sub["TTYPE%d" % i], fmt[code], shape))
-    dt = np.dtype(fields)
-    assert dt.itemsize == sub["NAXIS1"]
-    rec = np.frombuffer(buf, dtype=dt, count=sub["NAXIS2"], offset=pos)
-    return prim, sub, rec
+    """(primary header dict, SUBINT header dict, SUBINT records) of a PSRFITS
+    file: one written by :meth:`PSRFITS.save`, or the reference's template."""
+    hdus = read_fits(path)
+    sub, rec = hdus["SUBINT"]
+    return hdus["PRIMARY"][0], sub, rec
+
+
+def template_profile(path, subint=0, chan=0, pol=0, baseline="median"):
+    """Pulse profile of a fold-mode PSRFITS template: DATA * DAT_SCL +
+    DAT_OFFS of one (subint, channel, polarisation) -- the PSRFITS scaling
+    (template SUBINT: 'Data scale factor (outval=dataval*scl + offs)') -- as
+    float64 (NBIN,), with the baseline (the median bin; None: none) removed.
+    Config C4's portrait is this profile of the reference's B1855+09 template
+    (DataProfile of it, tiled over the channels)."""
+    _, sub, rec = read_psrfits(path)
+    npol = int(sub.get("NPOL", 1))
+    nchan = int(sub.get("NCHAN", 1))
+    r = rec[subint]
+    data = np.asarray(r["DATA"], dtype=np.float64).reshape(npol, nchan, -1)[pol, chan]
+    scl = np.asarray(r["DAT_SCL"], dtype=np.float64).reshape(-1)[pol * nchan + chan]
+    offs = np.asarray(r["DAT_OFFS"], dtype=np.float64).reshape(-1)[pol * nchan + chan]
+    prof = data * scl + offs
+    if baseline == "median":
+        prof = prof - np.median(prof)
+    return prof

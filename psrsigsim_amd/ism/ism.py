@@ -111,6 +111,7 @@ class ISM(object):
         Nph = pulsar._nph(signal)
         pulsar.Profiles.init_profiles(Nph, signal.Nchan)
         full_profs = pulsar.Profiles.calc_profiles(np.linspace(0.0, 1.0, Nph), signal.Nchan)
+        full_profs = np.array(full_profs)      # convolved per channel (a uniform table no longer is)
         t = np.linspace(0, pulsar._P(), Nph)
         tails = np.zeros((signal.Nchan, Nph))
         tau = np.atleast_1d(tau_scaled)

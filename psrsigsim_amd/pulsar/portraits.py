@@ -20,8 +20,45 @@ from .. import _lib
 
 log = logging.getLogger("psrsigsim_amd")
 
-__all__ = ["PulsePortrait", "GaussPortrait", "DataPortrait", "UserPortrait",
+__all__ = ["PulsePortrait", "GaussPortrait", "DataPortrait", "UserPortrait", "is_uniform", "rows_of",
            "pchip_slopes", "pchip_coefficients", "pchip_coefficients_np", "ppoly_eval", "ppoly_eval_np"]
+
+
+# ---------------------------------------------------------------------------
+# row-uniform tables
+#
+# A 1-D profile tiled over the channels (GaussProfile, DataProfile of a 1-D
+# template -- BASELINE configs C2-C5) gives an (Nchan, Nph) table whose rows
+# are all the same.  Such tables are kept as read-only broadcast views of
+# their one row (row stride 0) and every table operation below runs on that
+# row: the values are exactly those of the full table (each row is computed
+# by the same float64 operations), at 1/Nchan of the host time and memory.
+# ---------------------------------------------------------------------------
+def is_uniform(a):
+    """True for a broadcast table: 2-D, several rows, row stride 0."""
+    return isinstance(a, np.ndarray) and a.ndim >= 2 and a.shape[0] > 1 and a.strides[0] == 0
+
+
+def rows_of(a):
+    """The distinct rows to compute on: row 0 of a uniform table, else all."""
+    return a[:1] if is_uniform(a) else a
+
+
+def like_rows(res, a):
+    """``res`` (computed on rows_of(a)) with ``a``'s row count restored."""
+    if is_uniform(a) and res.shape[0] == 1:
+        return np.broadcast_to(res, (a.shape[0],) + res.shape[1:])
+    return res
+
+
+def tile_rows(row, nrows):
+    """np.tile(row, (nrows, 1)) as a uniform (broadcast) table."""
+    row = np.asarray(row)
+    return np.broadcast_to(row[None] if row.ndim == 1 else row[:1], (nrows,) + row.shape[-1:])
+
+
+def table_max(a):
+    return rows_of(a).max()
 
 
 # ---------------------------------------------------------------------------
@@ -63,8 +100,10 @@ def pchip_slopes(x, y, h=None, m=None):
 def pchip_coefficients(x, y):
     """Piecewise-cubic coefficients [rows, K-1, 4] in powers (t - x_i)^(3..0).
     Computed natively (pss_host_pchip_coef, one pass per row, host threads);
-    bitwise equal to :func:`pchip_coefficients_np`."""
-    return _lib.host_pchip_coef(x, np.atleast_2d(np.asarray(y, dtype=float)))
+    bitwise equal to :func:`pchip_coefficients_np`.  A uniform table's
+    coefficients are computed once and broadcast."""
+    y = np.atleast_2d(np.asarray(y, dtype=float))
+    return like_rows(_lib.host_pchip_coef(x, np.ascontiguousarray(rows_of(y))), y)
 
 
 def pchip_coefficients_np(x, y):
@@ -96,8 +135,8 @@ def ppoly_eval(x, c, ph, y=None):
     portraits.py:234 compares generator(0) with generator(1))."""
     ph = np.asarray(ph, dtype=float)
     if y is not None and ph.size <= x.size and np.array_equal(ph, x[:ph.size]):
-        return np.array(y[:, :ph.size])
-    return _lib.host_ppoly_eval(x, c, ph)
+        return like_rows(np.array(rows_of(y)[:, :ph.size]), y)
+    return like_rows(_lib.host_ppoly_eval(x, np.ascontiguousarray(rows_of(c)), ph), c)
 
 
 def ppoly_eval_np(x, c, ph):
@@ -122,10 +161,10 @@ def ppoly_eval_np(x, c, ph):
 def _first_max_row(profiles):
     """``[pr for pr in profiles if pr.max() == 1.0][0]`` (portraits.py:45),
     vectorised; IndexError when no row peaks at exactly 1.0, as there."""
-    hit = np.flatnonzero(np.max(profiles, axis=1) == 1.0)
+    hit = np.flatnonzero(np.max(rows_of(profiles), axis=1) == 1.0)
     if hit.size == 0:
         raise IndexError("list index out of range")
-    return profiles[hit[0]]
+    return rows_of(profiles)[hit[0]]
 
 
 class PulsePortrait(object):
@@ -143,8 +182,8 @@ class PulsePortrait(object):
         """portraits.py:32-45: sample at arange(N)/N, renormalise to max 1."""
         ph = np.arange(Nphase) / Nphase
         self._profiles = self.calc_profiles(ph, Nchan=Nchan)
-        self._Amax = self._profiles.max()
-        self._profiles = self._profiles / self.Amax
+        self._Amax = table_max(self._profiles)
+        self._profiles = like_rows(rows_of(self._profiles) / self.Amax, self._profiles)
         self._max_profile = _first_max_row(self._profiles)
 
     def calc_profiles(self, phases, Nchan=None):
@@ -217,9 +256,9 @@ class GaussPortrait(PulsePortrait):
                 one = _gauss_sum(ph, self.peak, self.width, self.amp)
             else:
                 one = _gauss_single(ph, self.peak, self.width, self.amp)
-            profiles = np.tile(one, (Nchan, 1))
-        self._Amax = self.Amax if hasattr(self, '_Amax') else np.amax(profiles)
-        return profiles / self._Amax
+            profiles = tile_rows(one, Nchan)
+        self._Amax = self.Amax if hasattr(self, '_Amax') else table_max(profiles)
+        return like_rows(rows_of(profiles) / self._Amax, profiles)
 
     @property
     def peak(self):
@@ -245,14 +284,19 @@ class DataPortrait(PulsePortrait):
 
     def __init__(self, profiles, phases=None):
         profiles = np.asarray(profiles)
-        neg = profiles < 0.0
+        uni = is_uniform(profiles)
+        work = rows_of(profiles)            # a uniform table is processed as its one row
+        neg = work < 0.0
         if np.any(neg):
             log.warning("Some phase bins of input profile are negative, replacing them with zeros...")
-            profiles[neg] = 0.0        # in place on the caller's array, as there
+            if uni:
+                work = np.where(neg, 0.0, work)
+            else:
+                work[neg] = 0.0            # in place on the caller's array, as there
         if phases is None:
-            N = profiles.shape[1]
-            if np.any(profiles[:, 0] != profiles[:, -1]):
-                profiles = np.append(profiles, profiles[:, 0][:, np.newaxis], axis=1)
+            N = work.shape[1]
+            if np.any(work[:, 0] != work[:, -1]):
+                work = np.append(work, work[:, 0][:, np.newaxis], axis=1)
                 phases = np.arange(N + 1) / N
             else:
                 phases = np.arange(N) / N
@@ -260,11 +304,14 @@ class DataPortrait(PulsePortrait):
             phases = np.asarray(phases, dtype=float)
             if phases[-1] != 1:
                 phases = np.append(phases, 1)
-                profiles = np.append(profiles, profiles[:, 0][:, np.newaxis], axis=1)
-            elif np.any(profiles[:, 0] != profiles[:, -1]):
-                profiles[:, -1] = profiles[:, 0]
+                work = np.append(work, work[:, 0][:, np.newaxis], axis=1)
+            elif np.any(work[:, 0] != work[:, -1]):
+                if uni:
+                    work = np.array(work)
+                work[:, -1] = work[:, 0]
         self._knots = np.asarray(phases, dtype=float)
-        self._kvals = np.asarray(profiles, dtype=float)
+        kv = np.asarray(work, dtype=float)
+        self._kvals = np.broadcast_to(kv, (profiles.shape[0],) + kv.shape[1:]) if uni else kv
         self._coef_cache = None
 
     @property
@@ -279,13 +326,13 @@ class DataPortrait(PulsePortrait):
     def _generator(self, phases):
         ph = np.asarray(phases, dtype=float)
         if ph.size <= self._knots.size and np.array_equal(ph, self._knots[:ph.size]):
-            return np.array(self._kvals[:, :ph.size])
+            return like_rows(np.array(rows_of(self._kvals)[:, :ph.size]), self._kvals)
         return ppoly_eval(self._knots, self._coef, phases, self._kvals)
 
     def calc_profiles(self, phases, Nchan=None):
         profiles = self._generator(phases)
-        Amax = self.Amax if hasattr(self, '_Amax') else np.max(profiles)
-        return profiles / Amax
+        Amax = self.Amax if hasattr(self, '_Amax') else table_max(profiles)
+        return like_rows(rows_of(profiles) / Amax, profiles)
 
     # -- device export --------------------------------------------------
     def uniform_knots(self):
@@ -308,7 +355,8 @@ class DataPortrait(PulsePortrait):
         h = 1.0 / M
         amax = self.Amax if hasattr(self, '_Amax') else 1.0
         # = (self._coef * [h**3, h**2, h, 1] / amax).astype(float32), natively
-        return _lib.host_device_table(self._coef, h, amax), M, nint
+        # (one row for a uniform table: the device then shares it)
+        return _lib.host_device_table(np.ascontiguousarray(rows_of(self._coef)), h, amax), M, nint
 
 
 class UserPortrait(PulsePortrait):

@@ -3,7 +3,7 @@ import logging
 
 import numpy as np
 
-from .portraits import PulsePortrait, GaussPortrait, DataPortrait, UserPortrait  # noqa: F401
+from .portraits import PulsePortrait, GaussPortrait, DataPortrait, UserPortrait, tile_rows  # noqa: F401
 
 log = logging.getLogger("psrsigsim_amd")
 
@@ -71,7 +71,7 @@ class DataProfile(DataPortrait):
         if profiles.ndim == 1:
             if Nchan is None:
                 Nchan = 1
-            profiles = np.tile(profiles, (Nchan, 1))
+            profiles = tile_rows(profiles, Nchan)     # np.tile, as a uniform (broadcast) table
         super().__init__(profiles=profiles, phases=phases)
 
     def set_Nchan(self, Nchan):

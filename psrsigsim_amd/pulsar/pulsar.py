@@ -13,7 +13,7 @@ import math
 import numpy as np
 
 from .profiles import GaussProfile, DataPortrait
-from .portraits import GaussPortrait
+from .portraits import GaussPortrait, is_uniform
 from .._units import make_quant, Quantity, to_value
 from .. import _engine
 
@@ -78,7 +78,12 @@ class Pulsar(object):
         Nph = self._nph(signal)
         self.Profiles.init_profiles(Nph, Nchan=signal.Nchan)
         full_profs = self.Profiles.calc_profiles(np.linspace(0.0, 1.0, Nph), Nchan=signal.Nchan)
-        full_profs *= C   # in place: a 1-row portrait with Nchan > 1 raises, as there
+        if is_uniform(full_profs) and np.all(C == 1.0):
+            pass          # x 1.0 is the identity: the uniform table stays one row
+        else:
+            if is_uniform(full_profs):
+                full_profs = np.array(full_profs)
+            full_profs *= C   # in place: a 1-row portrait with Nchan > 1 raises, as there
         self._Profiles = DataPortrait(full_profs)
 
     def make_pulses(self, signal, tobs):
@@ -238,6 +243,8 @@ class Pulsar(object):
 
 def _dedupe(tab):
     """One shared row when every channel's table is identical."""
+    if is_uniform(tab):
+        return np.ascontiguousarray(tab[0:1])
     if tab.shape[0] > 1 and np.all(tab == tab[0:1]):
         return np.ascontiguousarray(tab[0:1])
     return np.ascontiguousarray(tab)

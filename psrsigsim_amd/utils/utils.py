@@ -42,6 +42,8 @@ def shift_t(y, shift, dt=1):
             return torch.roll(y, shift, dims=-1)
         return np.roll(y, shift)
     t, was_np, was_1d = _as_rows(y)
+    if not was_np and t.data_ptr() == y.data_ptr():
+        t = t.clone()          # the reference returns a new array; y stays as it was
     R, N = t.shape
     s = np.broadcast_to(np.asarray(shift, dtype=np.float64) / float(dt), (R,))
     ramp = _engine.u64_to_i64_tensor(_engine.ramp_words(s, N))

@@ -359,6 +359,29 @@ def case_baseband():
     c.save()
 
 
+def case_simulate():
+    """Simulation.simulate (simulate/simulate.py:292-326) end to end with the
+    reference's own tests/test_simulate.py `simulation` fixture parameters
+    (430 MHz, 100 MHz, 64 channels, 2048e-6 MHz sampling, fold with 2-s
+    subints, P = 1 s, default Gaussian profile, tobs 4 s, DM 10, scattering
+    tau_d 50 ns @ 1500 MHz, TestScope 100 m / 5500 m^2 / 35 K, TestSys
+    backend 1.5625 MHz); the template-file argument is not used by
+    simulate(from_template=False)."""
+    from psrsigsim.simulate.simulate import Simulation
+    c = Case("simulate", 2023)
+    sim = Simulation(fcent=430, bandwidth=100, sample_rate=1.0 * 2048 * 10 ** -6, dtype=np.float32, Npols=1,
+                     Nchan=64, sublen=2.0, fold=True, period=1.0, Smean=1.0, profiles=None, tobs=4.0,
+                     name='J0000+0000', dm=10.0, tau_d=50e-9, tau_d_ref_f=1500.0, aperture=100.0, area=5500.0,
+                     Tsys=35.0, tscope_name="TestScope", system_name="TestSys", rcvr_fcent=430, rcvr_bw=100,
+                     rcvr_name="TestRCVR", backend_samprate=1.5625, backend_name="TestBack", tempfile=None,
+                     parfile=None, psrdict=None)
+    sim.simulate()
+    c.snap("final", sim.signal)
+    c.signal_meta(sim.signal)
+    c.meta["Amax"] = float(sim.pulsar.Profiles.Amax)
+    c.save()
+
+
 if __name__ == "__main__":
     if sys.argv[1:]:
         for name in sys.argv[1:]:
@@ -373,3 +396,4 @@ if __name__ == "__main__":
     case_observe_branches()
     case_utils()
     case_baseband()
+    case_simulate()

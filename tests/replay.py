@@ -76,8 +76,18 @@ for _tag, _dt in (("eq", 4.8828125e-06), ("down", 9.765625e-06), ("rebin", 7.5e-
 # ---------------------------------------------------------------------------
 # oracle interpretation (derives the injections)
 # ---------------------------------------------------------------------------
+def b1855():
+    """Config C4's portrait: the reference template's profile (io/psrfits.py
+    reader; DATA * DAT_SCL + DAT_OFFS, median baseline removed)."""
+    from psrsigsim_amd.io.psrfits import template_profile
+    from psrsigsim_amd.data import B1855_TEMPLATE
+    return template_profile(B1855_TEMPLATE)
+
+
 def _oracle_profile(spec):
     kind = spec[0]
+    if kind == "b1855":
+        return O.DataProfile(b1855(), nchan=spec[1])
     if kind == "gauss":
         return O.GaussPortrait(*spec[1:])
     if kind == "gaussarr":
@@ -102,7 +112,7 @@ def oracle_exec(case, d):
         sig.nchan = c1 - c0
     ps = case["psr"]
     pspec = ps["prof"]
-    if sg.get("chans") is not None and pspec[0] == "data":
+    if sg.get("chans") is not None and pspec[0] in ("data", "b1855"):
         pspec = ("data", sig.nchan)     # the same 1-D template on the shard's rows
     psr = O.Pulsar(ps["period"], ps["Smean"], profiles=_oracle_profile(pspec),
                    specidx=ps.get("specidx", 0.0), ref_freq=ps.get("ref_freq"))
@@ -227,6 +237,8 @@ def run_case(name, fused=True, case=None, seed=None):
         prof = GaussProfile(*spec[1:])
     elif spec[0] == "gaussarr":
         prof = GaussProfile(np.array([0.3, 0.6]), np.array([0.02, 0.05]), np.array([0.5, 1.0]))
+    elif spec[0] == "b1855":
+        prof = DataProfile(b1855(), Nchan=spec[1])
     else:
         prof = DataProfile(_prof(), Nchan=spec[1])
     psr = Pulsar(ps["period"], ps["Smean"], profiles=prof, specidx=ps.get("specidx", 0.0),

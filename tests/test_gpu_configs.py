@@ -167,7 +167,9 @@ def test_shift_t_odd_length(N, hip_lib):
     import torch
     x = torch.from_numpy(rng.random((3, N)).astype(np.float32)).cuda()
     shifts = np.array([1.5, -0.25, 100.125])
+    x0 = x.clone()
     out = shift_t(x, shifts, dt=1.0).cpu().numpy()
+    assert torch.equal(x, x0)              # a new array, as the reference returns
     assert out.shape == (3, N - 1)
     for r in range(3):
         ref = O.shift_t(x[r].cpu().numpy().astype(np.float64), float(shifts[r]), dt=1.0)

@@ -124,7 +124,7 @@ def test_fourstep_pair_path_vs_oracle(log2n, nchan, null, fused, hip_lib):
 F0_B1855 = 186.4940812499314404
 
 
-def _c4_case(nchan, null):
+def _c4_case(nchan, null, prof=None):
     """BASELINE config C4 (fold mode: 30 subints x 1024 bins = 30720 samples
     per channel, DM 13.3, radiometer noise) at a few channels: the
     mixed-radix four-step (30 x 1024) -- or, with a delayed null, the direct
@@ -135,12 +135,18 @@ def _c4_case(nchan, null):
     ops.append(("observe", "Arecibo", "Lband_PUPPI", True, "noise"))
     return dict(sig=dict(fcent=1400, bw=400, nchan=nchan, samprate=F0_B1855 * 1024 * 1e-6, sublen=60.0,
                          fold=True),
-                psr=dict(period=1.0 / F0_B1855, Smean=0.005, prof=("gauss", 0.5, 0.05, 1)), ops=ops)
+                psr=dict(period=1.0 / F0_B1855, Smean=0.005, prof=prof or ("gauss", 0.5, 0.05, 1)), ops=ops)
 
 
-@pytest.mark.parametrize("nchan,null", [(3, False), (4, False), (2, True)])
-def test_c4_fold_mixed_radix_vs_oracle(nchan, null, hip_lib):
-    errs = replay.run_case(None, fused=True, case=_c4_case(nchan, null), seed=nchan)
+@pytest.mark.parametrize("nchan,null,template", [(3, False, False), (4, False, False), (2, True, False),
+                                                  (4, False, True), (2, True, True)])
+def test_c4_fold_mixed_radix_vs_oracle(nchan, null, template, hip_lib):
+    """C4 with a Gaussian portrait and with the config's own B1855+09
+    template portrait (the reference's PSRFITS template read by
+    psrsigsim_amd.io.psrfits, resampled 2048 -> 1024 bins by the PCHIP
+    DataPortrait)."""
+    prof = ("b1855", nchan) if template else None
+    errs = replay.run_case(None, fused=True, case=_c4_case(nchan, null, prof), seed=nchan)
     bad = {k: v for k, v in errs.items() if not v <= TOL}
     assert not bad, errs
 

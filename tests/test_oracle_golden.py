@@ -224,3 +224,27 @@ def test_baseband():
         close(sig.data, A["data_disperse_" + tag], max(1e-9, 4 * maxph * 2.0 ** -53))
         with pytest.raises(ValueError):
             O.disperse_baseband(sig, dm)
+
+
+def _simulate_oracle(d):
+    """The reference's Simulation.simulate sequence (simulate.py:292-326) at
+    tests/test_simulate.py's `simulation` fixture parameters, on the oracle."""
+    sig = O.Signal(430, 100, nchan=64, samprate=1.0 * 2048 * 10 ** -6, sublen=2.0, fold=True)
+    psr = O.Pulsar(1.0, 1.0, profiles=O.GaussPortrait())     # profiles=None -> default Gaussian
+    O.scatter_broaden(sig, 50e-9, 1500.0, convolve=True, pulsar=psr)
+    O.make_pulses(sig, psr, 4.0, d)
+    O.disperse(sig, 10.0)
+    tel = O.Telescope(100.0, area=5500.0, Tsys=35.0)
+    tel.systems["TestSys"] = O.System(35.0, 1.5625)
+    out = O.observe(sig, psr, tel, "TestSys", d, noise=True)
+    return sig, psr, out
+
+
+def test_simulate():
+    """Simulation.simulate end to end, recorded from the reference
+    (tests/golden/make_golden.py case_simulate)."""
+    meta, A, draws = load("simulate")
+    sig, psr, _ = _simulate_oracle(O.InjectedDraws(draws))
+    assert sig.nsamp == meta["nsamp"] and sig.nsub == meta["nsub"]
+    assert np.isclose(sig.Smax, meta["Smax"], rtol=1e-12)
+    close(sig.data, A["data_final"], 1e-9)

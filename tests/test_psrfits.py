@@ -76,3 +76,59 @@ def test_psrfits_from_device_simulation(tmp_path, hip_lib):
     nbin = sub["NBIN"]
     assert nbin == 2048 and rec.shape == (3,)
     np.testing.assert_array_equal(rec["DATA"][2, 0], np.trunc(d[:, 2 * nbin:3 * nbin]).astype(np.int16))
+
+
+TEMPLATE = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.dirname(
+    __import__("os").path.abspath(__file__))), "data", "B1855+09.L-wide.PUPPI.11y.x.sum.sm")
+
+
+def test_read_reference_template():
+    """The reference's PSRFITS template (data/B1855+09.L-wide.PUPPI.11y.x.sum.sm,
+    config C4's portrait) parses: its HDUs, the SUBINT header and the int16
+    DATA with its scale/offset (outval = DATA * DAT_SCL + DAT_OFFS)."""
+    from psrsigsim_amd.io.psrfits import read_fits, template_profile
+    h = read_fits(TEMPLATE)
+    assert list(h) == ["PRIMARY", "HISTORY", "PSRPARAM", "POLYCO", "SUBINT"]
+    prim, _ = h["PRIMARY"]
+    sub, rec = h["SUBINT"]
+    assert prim["OBS_MODE"] == "PSR" and prim["SRC_NAME"] == "B1855+09"
+    assert sub["NBIN"] == 2048 and sub["NCHAN"] == 1 and sub["NPOL"] == 1 and sub["DM"] == 13.299393
+    assert rec.shape == (1,) and rec["DATA"].dtype == np.dtype(">i2") and rec["DATA"].shape == (1, 1, 1, 2048)
+    raw = rec["DATA"][0, 0, 0].astype(np.float64)
+    prof = template_profile(TEMPLATE, baseline=None)
+    np.testing.assert_array_equal(prof, raw * np.float64(rec["DAT_SCL"][0]) + np.float64(rec["DAT_OFFS"][0]))
+    p2 = template_profile(TEMPLATE)
+    assert abs(np.median(p2)) < 1e-12 and np.argmax(p2) == np.argmax(raw)
+    # the PSRPARAM table holds the pulsar frequency the reference reads (F0)
+    pp = h["PSRPARAM"][1]
+    lines = [bytes(x).decode().strip() for x in pp["PARAM"]]
+    assert lines[0].split() == ["PSR", "B1855+09"]
+    assert any(l.split()[0] in ("F0", "F") for l in lines)
+
+
+def test_writer_subint_layout_matches_template(tmp_path):
+    """The writer's SUBINT columns -- names, order, TFORM codes and repeat
+    counts, TDIM of DATA -- are the template's, at the template's geometry
+    (1 channel x 2048 bins), so the row layouts are identical."""
+    from psrsigsim_amd.io.psrfits import read_fits
+    rng = np.random.default_rng(3)
+    sig = _FakeSig(1, 2, 2048, rng)
+    path = str(tmp_path / "one.fits")
+    PSRFITS(path=path).save(sig, _FakePsr())
+    ours, rec = read_fits(path)["SUBINT"]
+    tmpl, trec = read_fits(TEMPLATE)["SUBINT"]
+    nf = int(tmpl["TFIELDS"])
+    assert int(ours["TFIELDS"]) == nf
+
+    def form(h, i):
+        f = str(h["TFORM%d" % i]).strip()
+        k = len(f) - len(f.lstrip("0123456789"))
+        return int(f[:k] or 1), f[k]
+    for i in range(1, nf + 1):
+        assert ours["TTYPE%d" % i] == tmpl["TTYPE%d" % i], i
+        assert form(ours, i) == form(tmpl, i), (i, ours["TTYPE%d" % i])
+    idx = [i for i in range(1, nf + 1) if tmpl["TTYPE%d" % i] == "DATA"][0]
+    assert ours["TDIM%d" % idx].replace(" ", "") == tmpl["TDIM%d" % idx].replace(" ", "")
+    assert rec.dtype == trec.dtype and ours["NAXIS1"] == tmpl["NAXIS1"]
+    for k in ("NBIN", "NCHAN", "NPOL", "NSBLK"):
+        assert ours[k] == tmpl[k], k

@@ -78,6 +78,27 @@ def test_save_errors():
 
 
 @pytest.mark.gpu
+def test_simulate_vs_reference_fixture(hip_lib):
+    """simulate() on the GPU with the reference's own recorded draws
+    injected, against the reference's Simulation.simulate output at its
+    tests/test_simulate.py `simulation` fixture parameters
+    (tests/golden/fixtures/simulate.*, recorded by make_golden.py)."""
+    import psrsigsim_amd as pss
+    from tests.fixtures_util import load
+    from tests.replay import _err
+    meta, A, draws = load("simulate")
+    sim = _sim()
+    pss.inject(gen=draws[0][2])
+    # the noise draws are consumed by observe(), the last stage
+    pss.inject(noise=draws[1][2])
+    sim.simulate()
+    got = sim.signal.data.cpu().numpy()
+    assert sim.signal.nsamp == meta["nsamp"] and got.shape == A["data_final"].shape
+    assert abs(float(sim.signal.Smax) / meta["Smax"] - 1) < 1e-12
+    assert _err(got, A["data_final"]) <= 1e-5
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("rate", [1.5625, 1.0 * 2048 * 10 ** -6], ids=["fixture", "2048bin"])
 def test_simulate_equals_manual_calls(rate, hip_lib):
     """simulate() = the reference's call sequence (simulate.py:292-326) made

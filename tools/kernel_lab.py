@@ -56,22 +56,27 @@ def main():
         L.pss_timing_enable(1)
         _lib.timing_collect()
         t0 = time.perf_counter()
+        spans = []
+        launches = []
         for _ in range(a.reps):
             s = step(v, a.nchan, a.log2n)
             _ = s.data
             del s
+            torch.cuda.synchronize()
+            spans.append(L.pss_timing_span_ms())      # device span of this step's runs
+            launches += _lib.timing_collect()
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / a.reps * 1e3
         L.pss_timing_enable(0)
         agg = {}
         full = a.nchan * (1 << a.log2n)
-        for kind, ms, u in _lib.timing_collect():
+        for kind, ms, u in launches:
             if u != full:
                 continue
             x = agg.setdefault(kind, [0.0, 0])
             x[0] += ms
             x[1] += 1
-        res[v] = {"wall_ms": round(wall, 2),
+        res[v] = {"wall_ms": round(wall, 2), "span_ms": round(sum(spans) / len(spans), 3),
                   **{k: round(x[0] / x[1], 3) for k, x in agg.items()}}
         print(v, json.dumps(res[v]), flush=True)
 
