@@ -137,10 +137,27 @@ struct Lds {
 template <int... Rs>
 struct RList {};
 
-template <int L, int BATCH, int T>
+// Synchronisation between the Stockham stages' LDS exchanges.  WAVE = true:
+// the transform belongs to ONE wave (T = 64 lanes, its own LDS region), so
+// the exchange only needs the wave's own LDS operations ordered -- no
+// s_barrier: the waves of a workgroup then run their transforms out of step
+// with each other, one wave's VALU work covering another's LDS latency.
+template <bool WAVE>
+__device__ __forceinline__ void stage_sync() {
+    if constexpr (WAVE) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+
+template <int L, int BATCH, int T, bool WAVE = false>
 struct Fft {
     static constexpr int E = L * BATCH / T;
     static_assert(E * T == L * BATCH, "T must divide L*BATCH");
+    static_assert(!WAVE || (T == 64 && BATCH == 1), "a wave-local transform is one sequence on 64 lanes");
 
     // Fill registers with the first-stage INPUT mapping of radix R0 from LDS.
     template <int R0>
@@ -226,10 +243,10 @@ struct Fft {
 #pragma unroll
                 for (int q = 0; q < R; ++q) lds[Lds<L>::at(b, base + q * Ns)] = v[ib * R + q];
             }
-            __syncthreads();
+            stage_sync<WAVE>();
             constexpr int R2 = first<Rest...>();
             load<R2>(v, lds, tid);
-            __syncthreads();
+            stage_sync<WAVE>();
             run<INV, Ns * R, Rest...>(v, lds, tid);
         }
     }

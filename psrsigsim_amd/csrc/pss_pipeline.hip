@@ -46,6 +46,16 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 #ifndef PSS_PHASE_WALK
 #define PSS_PHASE_WALK 1
 #endif
+// column FFTs of passes A / C wave-local (one wave per column, no workgroup
+// barriers between stages); experiment switch
+#ifndef PSS_WAVE_COLS
+#define PSS_WAVE_COLS 1
+#endif
+// delayed-null fix-up over the list of table words with nulls (1) or over
+// every word of every channel (0); experiment switch
+#ifndef PSS_NULL_LIST
+#define PSS_NULL_LIST 1
+#endif
 // cache policy bits of the column passes' spill loads (experiment switch;
 // gfx950 buffer aux: 1 = sc0, 2 = nt, 16 = sc1)
 #ifndef PSS_SPILL_AUX
@@ -141,6 +151,8 @@ struct KP {
     int mbB;                // column-block width B of pass C (mbits layout)
     const cf *rtab;         // [nchan][RFL] row-pass ramp factors (k_ramp_tab)
     hipEvent_t after_a;     // batching: recorded after this launch's pass A (or NULL)
+    const uint32_t *wlist;  // delayed null: table words with a nulled position (any f)
+    const uint32_t *nwlist; // its length (device)
 };
 
 // ---------------------------------------------------------------------------
@@ -345,6 +357,99 @@ __global__ __launch_bounds__(256) void k_null_fix(KP k) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             if ((h >> i) & 1u) row[n + i] = fmaf(nn, vn[i], vr[i] * sc);
+    }
+}
+
+// Table words (32 positions each) that hold a position nulled for some f:
+// the only words the null fix-up has to visit (the nulled pulses and their
+// Gibbs ringing, ~10-20% of the row).  Compacted once per run.
+__global__ __launch_bounds__(256) void k_mask_words(const uint2 *bits, uint32_t nwords, uint32_t *list,
+                                                    uint32_t *count) {
+    const uint32_t w = blockIdx.x * 256u + threadIdx.x;
+    bool nz = false;
+    if (w < nwords) {
+        const uint2 b = bits[w];
+        nz = (b.x | b.y) != 0u;
+    }
+    const uint64_t bal = __ballot(nz);
+    const int lane = threadIdx.x & 63;
+    uint32_t b0 = 0;
+    if (lane == 0 && bal) b0 = atomicAdd(count, (uint32_t)__popcll(bal));
+    b0 = __shfl(b0, 0);
+    if (nz) list[b0 + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = w;
+}
+
+// Delayed null fix-up driven by the word list: item (channel r, listed table
+// word w) covers data samples (32 w + i_c + j) mod N, j < 32 (the channel's
+// integer shift i_c carries table position p to sample p + i_c); the nulled
+// ones are rewritten as replacement + noise with the same Philox draws and
+// expression as epilogue4 (bitwise the generic kernels' values).  A sample
+// belongs to exactly one item, so items write disjoint samples; 4-sample
+// groups cut by an unaligned window are drawn by both neighbours, each
+// writing its own samples.  Grid-stride over the list (its length is only
+// known on the device).
+__global__ __launch_bounds__(256) void k_null_fix_list(KP k) {
+    __shared__ uint32_t desc[4][64 * 9];
+    __shared__ uint32_t dbase[4][64 * 9];
+    const int r = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const PssPipeline &p = k.p;
+    const uint32_t nl = *k.nwlist;
+    const uint32_t nm = (uint32_t)k.N - 1u;
+    uint32_t is;
+    float t;
+    mask_split((uint64_t)p.mask_ramp[r], k.log2n, is, t);
+    const uint32_t c = (uint32_t)(p.chan0 + r);
+    float *row = p.data + (int64_t)r * p.ld;
+    const Rng gn(p.seed, p.call_noise, P_NOISE), gr(p.seed, p.call_null, P_REP);
+    const float nn = p.noise_norm, sc = p.null_rep_scale;
+    const uint32_t stride = gridDim.x * 256u;
+    for (uint32_t i0 = blockIdx.x * 256u; i0 < nl; i0 += stride) {       // wave-uniform trip count
+        const uint32_t i = i0 + threadIdx.x;
+        uint32_t hits = 0, n0 = 0;
+        if (i < nl) {
+            const uint32_t w = k.wlist[i];
+            n0 = ((w << 5) + is) & nm;                   // data sample of table position 32 w
+            hits = mask_run(k, n0, is, t, 32u);
+        }
+        if (__ballot(hits != 0u) == 0ull) continue;
+        // (group, 4-bit mask) entries of this lane: samples n0 + j in groups
+        // of 4 aligned DATA indices (the Philox block of sample n is n >> 2)
+        const uint64_t below = (1ull << lane) - 1ull;
+        uint32_t total = 0;
+        const uint32_t a = n0 & 3u;                      // offset of n0 in its group
+        const uint64_t hx = (uint64_t)hits << a;         // hit bits by position in the aligned span
+#pragma unroll
+        for (int g = 0; g < 9; ++g) {
+            const uint32_t h = (uint32_t)(hx >> (4 * g)) & 15u;
+            const uint64_t bal = __ballot(h != 0u);
+            if (h) {
+                const uint32_t e = total + (uint32_t)__popcll(bal & below);
+                desc[wv][e] = h;
+                dbase[wv][e] = ((n0 - a) + 4u * (uint32_t)g) & nm;   // first sample of the group
+            }
+            total += (uint32_t)__popcll(bal);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t e = (uint32_t)lane; e < total; e += 64u) {
+            const uint32_t h = desc[wv][e], nb = dbase[wv][e];
+            const float4 xn = chi2_1x4(gn.bits(nb >> 2, c, 0u));
+            const float4 xr = chi2_1x4(gr.bits(nb >> 2, c, 0u));
+            const float vn[4] = {xn.x, xn.y, xn.z, xn.w}, vr[4] = {xr.x, xr.y, xr.z, xr.w};
+            if (h == 15u) {
+                *reinterpret_cast<float4 *>(row + nb) =
+                    make_float4(fmaf(nn, vn[0], vr[0] * sc), fmaf(nn, vn[1], vr[1] * sc),
+                                fmaf(nn, vn[2], vr[2] * sc), fmaf(nn, vn[3], vr[3] * sc));
+                continue;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if ((h >> q) & 1u) row[nb + q] = fmaf(nn, vn[q], vr[q] * sc);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
@@ -1125,6 +1230,11 @@ template <int N1, int B, int T, int... F, int... I>
 struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
     using FF = Fft<N1, B, T>;
     static constexpr int E = FF::E;
+    // One wave per column (T = 64 B, N1/64 values per lane): the column FFTs
+    // are wave-local (Fft<..., WAVE>: no workgroup barrier between stages);
+    // only the transposes between sample-major items and columns need one.
+    using FW = Fft<(N1 % 64 == 0 ? N1 : 64), 1, 64, true>;     // (a placeholder when N1 % 64 != 0)
+    static constexpr bool kWaveCols = PSS_WAVE_COLS && (T == 64 * B) && (N1 % 64 == 0) && (N1 / 64 == E);
     static constexpr int RF0 = FF::template first<F...>();
     static constexpr int RFL = FF::template last_of<F...>();
     static constexpr int RI0 = FF::template first<I...>();
@@ -1251,21 +1361,40 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         }
         __syncthreads();
         cf v[E];
-        FF::template load<RF0>(v, lds, tid);
-        __syncthreads();
-        if constexpr (!(kAbl & 2)) FF::template run<false, 1, F...>(v, lds, tid);
         const float invN = k.invN;
+        if constexpr (kWaveCols) {
+            // wave w transforms column w in its own LDS row
+            const int wv = tid >> 6, lane = tid & 63;
+            cf *wl = lds + wv * Lds<N1>::RS;
+            FW::template load<RF0>(v, wl, lane);
+            stage_sync<true>();
+            if constexpr (!(kAbl & 2)) FW::template run<false, 1, F...>(v, wl, lane);
 #pragma unroll
-        for (int i = 0; i < E; ++i) {
-            int b, k1;
-            FF::template where<RFL>(i, tid, b, k1);
-            // (n20 + b) k1 < N1 N2 = N <= 2^24: exact in 32-bit and in float
-            const uint32_t m = (uint32_t)(n20 + b) * (uint32_t)k1;
-            float rev = (float)m * invN;
-            if (rev >= 0.5f) rev -= 1.0f;
-            if constexpr (!(kAbl & 4)) v[i] = cmul(v[i], expi_rev(-rev)); else v[i] = v[i];
+            for (int i = 0; i < E; ++i) {
+                int b0, k1;
+                FW::template where<RFL>(i, lane, b0, k1);
+                const uint32_t m = (uint32_t)(n20 + wv) * (uint32_t)k1;
+                float rev = (float)m * invN;
+                if (rev >= 0.5f) rev -= 1.0f;
+                if constexpr (!(kAbl & 4)) v[i] = cmul(v[i], expi_rev(-rev)); else v[i] = v[i];
+            }
+            FW::template store<RFL>(v, wl, lane);
+        } else {
+            FF::template load<RF0>(v, lds, tid);
+            __syncthreads();
+            if constexpr (!(kAbl & 2)) FF::template run<false, 1, F...>(v, lds, tid);
+#pragma unroll
+            for (int i = 0; i < E; ++i) {
+                int b, k1;
+                FF::template where<RFL>(i, tid, b, k1);
+                // (n20 + b) k1 < N1 N2 = N <= 2^24: exact in 32-bit and in float
+                const uint32_t m = (uint32_t)(n20 + b) * (uint32_t)k1;
+                float rev = (float)m * invN;
+                if (rev >= 0.5f) rev -= 1.0f;
+                if constexpr (!(kAbl & 4)) v[i] = cmul(v[i], expi_rev(-rev)); else v[i] = v[i];
+            }
+            FF::template store<RFL>(v, lds, tid);
         }
-        FF::template store<RFL>(v, lds, tid);
         __syncthreads();
         cf *Y = k.Yd + (int64_t)pr * k.N;
         for (int it = tid; it < N1 * B / 4; it += T) {
@@ -1320,10 +1449,19 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         }
         __syncthreads();
         cf v[E];
-        FF::template load<RI0>(v, lds, tid);
-        __syncthreads();
-        if constexpr (!(kAbl & 2)) FF::template run<true, 1, I...>(v, lds, tid);
-        FF::template store<RIL>(v, lds, tid);
+        if constexpr (kWaveCols) {
+            const int wv = tid >> 6, lane = tid & 63;
+            cf *wl = lds + wv * Lds<N1>::RS;
+            FW::template load<RI0>(v, wl, lane);
+            stage_sync<true>();
+            if constexpr (!(kAbl & 2)) FW::template run<true, 1, I...>(v, wl, lane);
+            FW::template store<RIL>(v, wl, lane);
+        } else {
+            FF::template load<RI0>(v, lds, tid);
+            __syncthreads();
+            if constexpr (!(kAbl & 2)) FF::template run<true, 1, I...>(v, lds, tid);
+            FF::template store<RIL>(v, lds, tid);
+        }
         __syncthreads();
     }
 
@@ -2070,7 +2208,7 @@ static BsGeom bs_geom(int32_t nchan, int64_t N) {
 }
 
 struct WsLayout {
-    int64_t yd, mspec, ynode, nodes, bits, base, coef, misc, mbits, rtab, row, total;
+    int64_t yd, mspec, ynode, nodes, bits, base, coef, misc, mbits, rtab, wlist, row, total;
     int64_t bs_chirp, bs_bhat, bs_z;   // Bluestein: w [N] | Bhat [M] | Z [nb][M] (cf)
     int64_t odd_tw;                    // odd N: exp(+2 pi i j / (N - 1)), j < N - 1 (cf)
 };
@@ -2091,6 +2229,7 @@ static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
         w.misc = o;  o += 256;
         w.mbits = o; o += al256((int64_t)nchan * (N / 8));   // per-channel null bits
         w.rtab = o;  o += al256((int64_t)nchan * 64 * 8);     // row-pass ramp factors (RFL <= 64)
+        w.wlist = o; o += al256((N / 32) * 4);                 // null fix-up: table words with nulls
     } else if (filt || !(is_pow2(N) && N >= 64 && N <= 8192)) {
         // fallback: W1, W2, twiddles -- Bluestein needs W1 only (its forward
         // and inverse DFTs are fused through Z), unless the mixed-radix
@@ -2197,6 +2336,16 @@ static int build_mask_table(KP &k, hipStream_t st, const float *mask_row, char *
         nodes, k.N, reinterpret_cast<uint2 *>(w + L.bits), reinterpret_cast<uint32_t *>(w + L.base),
         reinterpret_cast<float *>(w + L.coef), counter);
     LAUNCHCHK();
+    {
+        uint32_t *wl = reinterpret_cast<uint32_t *>(w + L.wlist);
+        uint32_t *wcount = reinterpret_cast<uint32_t *>(w + L.misc + 8);
+        HIPCHK(hipMemsetAsync(wcount, 0, 4, st));
+        const uint32_t nwords = (uint32_t)(k.N / 32);
+        k_mask_words<<<dim3((nwords + 255) / 256), dim3(256), 0, st>>>(k.mt_bits, nwords, wl, wcount);
+        LAUNCHCHK();
+        k.wlist = wl;
+        k.nwlist = wcount;
+    }
     k.mtab = 1;
     k.log2n = log2n;
     if (k.p.data_in_fft && !fast_epilogue(k)) {   // generic pass C reads the decisions as bits
@@ -2373,7 +2522,13 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     LAUNCHCHK();
     if (fast && k.mtab) {
         tk_begin(TK_NULLFIX, st);
-        k_null_fix<<<dim3((unsigned)((k.N / 32 + 255) / 256), (unsigned)k.p.nchan), dim3(256), 0, st>>>(k);
+        if (PSS_NULL_LIST) {
+            // grid-stride over the word list: ~1/8 of the words per channel
+            const unsigned gx = (unsigned)((k.N / 32 / 8 + 255) / 256);
+            k_null_fix_list<<<dim3(gx ? gx : 1, (unsigned)k.p.nchan), dim3(256), 0, st>>>(k);
+        } else {
+            k_null_fix<<<dim3((unsigned)((k.N / 32 + 255) / 256), (unsigned)k.p.nchan), dim3(256), 0, st>>>(k);
+        }
         tk_end(st);
         LAUNCHCHK();
     }
