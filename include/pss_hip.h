@@ -158,6 +158,13 @@ typedef struct PssPipeline {
     const int64_t *null_shift_dev;  /* NULL: use null_shift; else the device
                                word pss_null_shift wrote (shift_val computed on
                                the device, no host round trip)                */
+    const float *tail_a;    /* [nchan] scattering tail (extension, no reference
+                               counterpart -- SURVEY App. A.11): circular
+                               convolution of each row with the normalised
+                               exponential h[n] = (1-a) a^n, a = exp(-dt/tau_c),
+                               i.e. bin k x H(k) = (1-a) / (1 - a e^{-2 pi i k/N})
+                               in the same forward/inverse pass as the delay
+                               ramp; NULL = none                             */
 } PssPipeline;
 
 /* Library / device info. */

@@ -190,12 +190,13 @@ class Pending(object):
     def __init__(self, source=None):
         self.source = source          # None -> load existing data
         self.shifts = []              # list of np.float64 [Nchan_global] (samples)
+        self.tail = None              # np.float64 [Nchan_global] scattering-tail a (extension)
         self.null = None              # dict
         self.noise = None             # dict
         self.out = None               # dict(kind, tensor, clip)
 
     def empty(self):
-        return (self.source is None and not self.shifts and self.null is None
+        return (self.source is None and not self.shifts and self.tail is None and self.null is None
                 and self.noise is None and self.out is None)
 
 
@@ -219,7 +220,7 @@ def plan_pipeline(sig, pend, rows, chan0):
         if src.inj is not None:
             A["inj_gen"] = inj_rows(src.inj, gidx)
     nul = pend.null
-    need_fft = bool(pend.shifts) or (nul is not None and nul["mode"] == "delayed")
+    need_fft = bool(pend.shifts) or pend.tail is not None or (nul is not None and nul["mode"] == "delayed")
     if need_fft:
         if N % 2:
             raise ValueError("could not broadcast input array from shape (%d,) into shape (%d,)"
@@ -234,7 +235,7 @@ def plan_pipeline(sig, pend, rows, chan0):
             mask_total = nul["mask_samples"]
             nyq_im = np.cos(np.pi * mask_total)
             A["mask_ramp"] = ramp_words(mask_total[gidx], N)
-            if pend.shifts:
+            if pend.shifts or pend.tail is not None:
                 P["data_in_fft"], ramp_s = 1, total
             else:
                 P["data_in_fft"], ramp_s = 0, mask_total
@@ -243,6 +244,8 @@ def plan_pipeline(sig, pend, rows, chan0):
         A["ramp"] = ramp_words(ramp_s[gidx], N)
         A["nyq_re"] = nyq_re[gidx].astype(np.float32)
         A["nyq_im"] = nyq_im[gidx].astype(np.float32)
+        if pend.tail is not None:
+            A["tail_a"] = pend.tail[gidx].astype(np.float32)
     if nul is not None:
         P.update(null_mode=_lib.NULL_DELAYED if nul["mode"] == "delayed" else _lib.NULL_UNDELAYED,
                  null_slots=int(nul["rank"].size), null_shift=int(nul.get("shift_val", 0)),
@@ -375,6 +378,7 @@ def null_shift_device(sig, pend, count):
             scratch.copy_(base)
         probe = Pending(pend.source)
         probe.shifts = list(pend.shifts)
+        probe.tail = pend.tail
         probe.null = pend.null
         p, keep = build_pipeline(sig, probe, nrow, 0, scratch, ws_role="probe")
         run(p, keep)

@@ -14,10 +14,8 @@
 // the row kernel fuses forward FFT -> ramp -> inverse FFT without touching LDS
 // in between.
 //
-// LDS layout: sequence b at row offset b*RS (RS = L + L/16 + 1 complex); inside
-// a row position p lives at p + (p >> 4).  The intra-row pad breaks the
-// stride-16 Stockham scatter; the odd row pitch breaks the cross-row transposes
-// of the column kernels (see DESIGN.md "LDS layout").
+// LDS layout: sequence b at row offset b*RS; inside a row an XOR swizzle per
+// aligned 16-complex block (Lds below; DESIGN.md "LDS layout").
 #pragma once
 #include "pss_device.hpp"
 
@@ -127,10 +125,26 @@ __device__ __forceinline__ void dft(cf *a) {
     }
 }
 
-template <int L>
+// LDS layout of BATCH sequences of length L.  L % 16 == 0: position p of a
+// row lives at p ^ ((p >> 4) & 15) -- an XOR swizzle inside each aligned
+// 16-complex block, so the stride-16 Stockham scatters spread over the banks
+// while contiguous reads of 32 positions stay one aligned 64-dword block
+// (the round-1 pad of one complex per 16 made every such read wrap onto two
+// banks: 2x the cycles, tools/lds_banks.py); row pitch RS = L + XRS, XRS
+// chosen per kernel for its cross-row (transposing) accesses.  Other L (the
+// mixed-radix columns 6..60): pad of one complex per 16.
+#ifndef PSS_LDS_PAD
+#define PSS_LDS_PAD 0      // experiment switch: 1 = the round-1 padded layout everywhere
+#endif
+template <int L, int XRS = 1>
 struct Lds {
-    static constexpr int RS = L + L / 16 + 1;   // row pitch (complex)
-    __device__ static __forceinline__ int at(int b, int p) { return b * RS + p + (p >> 4); }
+    // XRS < 0: the padded layout (a kernel whose accesses it suits better)
+    static constexpr bool SWZ = (L % 16) == 0 && !PSS_LDS_PAD && XRS >= 0;
+    static constexpr int RS = SWZ ? L + XRS : L + L / 16 + 1;   // row pitch (complex)
+    __device__ static __forceinline__ int at(int b, int p) {
+        if constexpr (SWZ) return b * RS + (p ^ ((p >> 4) & 15));
+        else return b * RS + p + (p >> 4);
+    }
     static constexpr int bytes(int batch) { return batch * RS * 8; }
 };
 
@@ -153,8 +167,9 @@ __device__ __forceinline__ void stage_sync() {
     }
 }
 
-template <int L, int BATCH, int T, bool WAVE = false>
+template <int L, int BATCH, int T, bool WAVE = false, int XRS = 1>
 struct Fft {
+    using LD = Lds<L, XRS>;
     static constexpr int E = L * BATCH / T;
     static_assert(E * T == L * BATCH, "T must divide L*BATCH");
     static_assert(!WAVE || (T == 64 && BATCH == 1), "a wave-local transform is one sequence on 64 lanes");
@@ -167,7 +182,7 @@ struct Fft {
         for (int ib = 0; ib < E / R0; ++ib) {
             const int j = tid + ib * T, b = j / LR, jj = j - b * LR;
 #pragma unroll
-            for (int q = 0; q < R0; ++q) v[ib * R0 + q] = lds[Lds<L>::at(b, jj + q * LR)];
+            for (int q = 0; q < R0; ++q) v[ib * R0 + q] = lds[LD::at(b, jj + q * LR)];
         }
     }
     // Store registers (last-stage OUTPUT mapping of radix R) to LDS, natural.
@@ -178,7 +193,7 @@ struct Fft {
         for (int ib = 0; ib < E / R; ++ib) {
             const int j = tid + ib * T, b = j / LR, jj = j - b * LR;
 #pragma unroll
-            for (int q = 0; q < R; ++q) lds[Lds<L>::at(b, jj + q * LR)] = v[ib * R + q];
+            for (int q = 0; q < R; ++q) lds[LD::at(b, jj + q * LR)] = v[ib * R + q];
         }
     }
     // (b, position) of register i under the natural mapping of radix R.
@@ -241,7 +256,7 @@ struct Fft {
                 const int k = jj % Ns;
                 const int base = (jj / Ns) * Ns * R + k;
 #pragma unroll
-                for (int q = 0; q < R; ++q) lds[Lds<L>::at(b, base + q * Ns)] = v[ib * R + q];
+                for (int q = 0; q < R; ++q) lds[LD::at(b, base + q * Ns)] = v[ib * R + q];
             }
             stage_sync<WAVE>();
             constexpr int R2 = first<Rest...>();

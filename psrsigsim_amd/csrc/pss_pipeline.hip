@@ -763,9 +763,34 @@ __global__ __launch_bounds__(256) void k_box_row(KP k, float *row) {
     }
 }
 
+__device__ __forceinline__ cf apply_ramp_delay(const KP &k, int r, int64_t kb, cf z);
+
+// Scattering-tail transfer function of row r at bin kb (extension, see
+// PssPipeline.tail_a): H = (1 - a) / (1 - a e^{-2 pi i kb/N}); exactly 1 at DC
+// and real (1-a)/(1+a) at Nyquist, Hermitian in kb, so irfft stays real.
+__device__ __forceinline__ cf tail_factor(float a, cf w) {
+    // w = e^{-2 pi i kb / N}; 1/(1 - a w) = conj(d) / |d|^2, d = 1 - a w
+    const float dr = fmaf(-a, w.x, 1.0f), di = -a * w.y;
+    const float s = (1.0f - a) / fmaf(dr, dr, di * di);
+    return make_float2(dr * s, -di * s);
+}
+__device__ __forceinline__ cf bin_phasor(int64_t kb, int64_t N) {
+    const int64_t kk = (2 * kb > N) ? kb - N : kb;
+    return expi_rev(-(float)((double)kk / (double)N));
+}
+
 // exp(-2 pi i k' s / N) for frequency bin k, with the reference's Nyquist
 // rule applied separately to the real (data) and imaginary (mask) parts.
 __device__ __forceinline__ cf apply_ramp(const KP &k, int r, int64_t kb, cf z) {
+    if (k.p.tail_a && !k.p.htab) {
+        const cf h = tail_factor(k.p.tail_a[r], bin_phasor(kb, k.N));
+        const cf t = apply_ramp_delay(k, r, kb, z);
+        if (kb == 0 || 2 * kb == k.N) return make_float2(t.x * h.x, t.y * h.x);   // real parts only
+        return cmul(t, h);
+    }
+    return apply_ramp_delay(k, r, kb, z);
+}
+__device__ __forceinline__ cf apply_ramp_delay(const KP &k, int r, int64_t kb, cf z) {
     const PssPipeline &p = k.p;
     const int64_t N = k.N;
     if (p.htab) {
@@ -1107,7 +1132,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
     // MASK = false: data pair of channels (2pr - poff, 2pr + 1 - poff).
     // MASK = true : node pair (2pr, 2pr + 1) of the mask table build -- the
     //               once-per-run mask spectrum times each node's ramp.
-    template <bool MASK>
+    template <bool MASK, bool TAIL = false>
     __device__ static void pass(const KP &k) {
         __shared__ cf lds[2 * Lds<N2>::RS];
         const int tid = threadIdx.x;
@@ -1157,13 +1182,25 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                     if constexpr (kAbl & 8) {
                         v[i] = cadd(Sa, Sb);
                     } else if (kb0 == 0 && 2 * q == RFL) {          // Nyquist bin
-                        v[i] = make_float2((0.5f * Sa.x) * k.p.nyq_re[ra], (0.5f * Sb.x) * k.p.nyq_re[rb]);
-                    } else if (kb0 == 0 && q == 0) {                // DC
+                        float fa = k.p.nyq_re[ra], fb = k.p.nyq_re[rb];
+                        if constexpr (TAIL) {                       // H(N/2) = (1-a)/(1+a)
+                            const float ta = k.p.tail_a[ra], tb = k.p.tail_a[rb];
+                            fa *= (1.0f - ta) / (1.0f + ta);
+                            fb *= (1.0f - tb) / (1.0f + tb);
+                        }
+                        v[i] = make_float2((0.5f * Sa.x) * fa, (0.5f * Sb.x) * fb);
+                    } else if (kb0 == 0 && q == 0) {                // DC (H = 1)
                         const cf Da = make_float2(0.5f * Sa.x, 0.5f * Sa.y), Db = make_float2(0.5f * Sb.x, 0.5f * Sb.y);
                         v[i] = make_float2(Da.x - Db.y, Da.y + Db.x);
                     } else {
-                        const cf A = cmul(Sa, cmul(ba, k.rtab[(int64_t)ra * RFL + q]));
-                        const cf Bv = cmul(Sb, cmul(bb, k.rtab[(int64_t)rb * RFL + q]));
+                        cf ra_ = cmul(ba, k.rtab[(int64_t)ra * RFL + q]), rb_ = cmul(bb, k.rtab[(int64_t)rb * RFL + q]);
+                        if constexpr (TAIL) {
+                            const cf w = bin_phasor(kb0 + (int64_t)q * (k.N / RFL), k.N);
+                            ra_ = cmul(ra_, tail_factor(k.p.tail_a[ra], w));
+                            rb_ = cmul(rb_, tail_factor(k.p.tail_a[rb], w));
+                        }
+                        const cf A = cmul(Sa, ra_);
+                        const cf Bv = cmul(Sb, rb_);
                         v[i] = make_float2(A.x - Bv.y, A.y + Bv.x);
                     }
                 }
@@ -1217,18 +1254,21 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
     }
 };
 
-template <typename R, int T>
-__global__ __launch_bounds__(T, (T <= 512 ? 2 * T / 256 : 4)) void k_pair_row(KP k) { R::template pass<false>(k); }
+template <typename R, int T, bool TAIL = false>
+__global__ __launch_bounds__(T, (T <= 512 ? 2 * T / 256 : 4)) void k_pair_row(KP k) { R::template pass<false, TAIL>(k); }
 template <typename R, int T>
 __global__ __launch_bounds__(T) void k_node_row(KP k) { R::template pass<true>(k); }
 
 
-template <int N1, int B, int T, typename FWD, typename INV>
+// XRS: extra row pitch of the LDS column block (Lds), chosen per kernel for
+// its transposing accesses (xrs_read / xrs_write below).
+template <int N1, int B, int T, typename FWD, typename INV, int XRS = 1>
 struct PairCols;
 
-template <int N1, int B, int T, int... F, int... I>
-struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
-    using FF = Fft<N1, B, T>;
+template <int N1, int B, int T, int... F, int... I, int XRS>
+struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
+    using LdsC = Lds<N1, XRS>;
+    using FF = Fft<N1, B, T, false, XRS>;
     static constexpr int E = FF::E;
     // One wave per column (T = 64 B, N1/64 values per lane): the column FFTs
     // are wave-local (Fft<..., WAVE>: no workgroup barrier between stages);
@@ -1250,7 +1290,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
     // injected draws, no undelayed null -- the same values as source4.
     template <bool FAST, bool SHARED = false>
     __device__ static void passA(const KP &k) {
-        __shared__ cf lds[B * Lds<N1>::RS];
+        __shared__ cf lds[B * LdsC::RS];
         const int tid = threadIdx.x;
         int cbx, pr;
         xcd_block(cbx, pr);
@@ -1290,9 +1330,19 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
 #endif
 #pragma unroll
             for (int t = 0; t < ITEMS; ++t) {
+                // items along the column (lanes = consecutive rows n1 of one
+                // 4-column group): the transposed LDS writes below are
+                // conflict-free for any row pitch (this loop touches no
+                // global memory, so its item order is free)
                 const int it = tid + t * T;
-                const int n1 = it / (B / 4);
-                const int b4 = (it - n1 * (B / 4)) * 4;
+                int n1, b4;
+                if constexpr (N1 % 64 == 0) {
+                    n1 = it % N1;
+                    b4 = (it / N1) * 4;
+                } else {
+                    n1 = it / (B / 4);
+                    b4 = (it - n1 * (B / 4)) * 4;
+                }
                 const uint32_t n = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4;   // N <= 2^24
                 const float4 qa = chi2_1x4(g.bits(n >> 2, ca, 0u));
                 const float4 qb = chi2_1x4(g.bits(n >> 2, cb, 0u));
@@ -1319,7 +1369,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
                         pb = fmaf(fmaf(fmaf(Bc.x, u, Bc.y), u, Bc.z), u, Bc.w);
                     }
                     const float xa = pa * va[i] * dn, xb = pb * vb[i] * dn;
-                    lds[Lds<N1>::at(b4 + i, n1)] = make_float2(hasa ? xa : 0.f, hasb ? xb : 0.f);
+                    lds[LdsC::at(b4 + i, n1)] = make_float2(hasa ? xa : 0.f, hasb ? xb : 0.f);
                 }
             }
         } else
@@ -1357,7 +1407,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
             else { xb[0] = xb[1] = xb[2] = xb[3] = 0.f; }
             }
 #pragma unroll
-            for (int i = 0; i < 4; ++i) lds[Lds<N1>::at(b4 + i, n1)] = make_float2(xa[i], xb[i]);
+            for (int i = 0; i < 4; ++i) lds[LdsC::at(b4 + i, n1)] = make_float2(xa[i], xb[i]);
         }
         __syncthreads();
         cf v[E];
@@ -1365,7 +1415,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         if constexpr (kWaveCols) {
             // wave w transforms column w in its own LDS row
             const int wv = tid >> 6, lane = tid & 63;
-            cf *wl = lds + wv * Lds<N1>::RS;
+            cf *wl = lds + wv * LdsC::RS;
             FW::template load<RF0>(v, wl, lane);
             stage_sync<true>();
             if constexpr (!(kAbl & 2)) FW::template run<false, 1, F...>(v, wl, lane);
@@ -1400,8 +1450,8 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
         for (int it = tid; it < N1 * B / 4; it += T) {
             const int k1 = it / (B / 4);
             const int b4 = (it - k1 * (B / 4)) * 4;
-            cf a0 = lds[Lds<N1>::at(b4 + 0, k1)], a1 = lds[Lds<N1>::at(b4 + 1, k1)];
-            cf a2 = lds[Lds<N1>::at(b4 + 2, k1)], a3 = lds[Lds<N1>::at(b4 + 3, k1)];
+            cf a0 = lds[LdsC::at(b4 + 0, k1)], a1 = lds[LdsC::at(b4 + 1, k1)];
+            cf a2 = lds[LdsC::at(b4 + 2, k1)], a3 = lds[LdsC::at(b4 + 3, k1)];
             float4 *dst = reinterpret_cast<float4 *>(Y + (int64_t)k1 * N2 + n20 + b4);
             dst[0] = make_float4(a0.x, a0.y, a1.x, a1.y);
             dst[1] = make_float4(a2.x, a2.y, a3.x, a3.y);
@@ -1409,7 +1459,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
     }
 
     // inverse column FFTs of one spilled pair block; result left in LDS in
-    // natural order (Lds<N1>::at(column, n1)), unscaled.  The load loop is
+    // natural order (LdsC::at(column, n1)), unscaled.  The load loop is
     // deliberately rolled: with every load of the block in flight at once
     // (64 KB per workgroup) the column passes overflow the XCD's L2 and the
     // half-line reads / 32-B output segments of neighbouring blocks stop
@@ -1444,14 +1494,14 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
             const cf tw[4] = {w0, cmul(w0, w1), cmul(w0, w2), cmul(w0, cmul(w2, w1))};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                if constexpr (!(kAbl & 4)) lds[Lds<N1>::at(b4 + i, k1)] = cmul(a[i], tw[i]); else lds[Lds<N1>::at(b4 + i, k1)] = a[i];
+                if constexpr (!(kAbl & 4)) lds[LdsC::at(b4 + i, k1)] = cmul(a[i], tw[i]); else lds[LdsC::at(b4 + i, k1)] = a[i];
             }
         }
         __syncthreads();
         cf v[E];
         if constexpr (kWaveCols) {
             const int wv = tid >> 6, lane = tid & 63;
-            cf *wl = lds + wv * Lds<N1>::RS;
+            cf *wl = lds + wv * LdsC::RS;
             FW::template load<RI0>(v, wl, lane);
             stage_sync<true>();
             if constexpr (!(kAbl & 2)) FW::template run<true, 1, I...>(v, wl, lane);
@@ -1468,7 +1518,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
     // C: inverse column FFTs of the data pair, then the epilogues of channels
     // a, b straight from LDS (delayed-null decisions from the mask table).
     __device__ static void passC(const KP &k) {
-        __shared__ cf lds[B * Lds<N1>::RS];
+        __shared__ cf lds[B * LdsC::RS];
         const int tid = threadIdx.x;
         int cbx, pr;
         xcd_block(cbx, pr);
@@ -1488,7 +1538,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
             const uint32_t hb = (mask && hasb) ? mask_bits4<B, N1>(k, rb, cbx, n1, b4) : 0u;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const cf z = lds[Lds<N1>::at(b4 + i, n1)];
+                const cf z = lds[LdsC::at(b4 + i, n1)];
                 da[i] = z.x * invN;
                 db[i] = z.y * invN;
                 ma[i] = ((ha >> i) & 1u) ? 2.0f : 0.0f;
@@ -1507,7 +1557,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
     // samples; scattered 8192 apart in this kernel's column order).
     __device__ static void passC_fast(const KP &k) {
         static_assert(kItemsExact, "fast pass C: whole items per thread");
-        __shared__ __align__(16) cf lds[B * Lds<N1>::RS];
+        __shared__ __align__(16) cf lds[B * LdsC::RS];
         const int tid = threadIdx.x;
         int cbx, pr;
         xcd_block(cbx, pr);
@@ -1541,7 +1591,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
             const float na[4] = {xa.x, xa.y, xa.z, xa.w}, nb[4] = {xb.x, xb.y, xb.z, xb.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const cf z = lds[Lds<N1>::at(b4 + i, n1)];
+                const cf z = lds[LdsC::at(b4 + i, n1)];
                 acc[t][0][i] = fmaf(nn, na[i], z.x * invN);
                 acc[t][1][i] = fmaf(nn, nb[i], z.y * invN);
             }
@@ -1566,7 +1616,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
     // Mask table build: inverse column FFTs of node pair `blockIdx.y`, stored
     // (scaled) as node rows nodes[2 pr], nodes[2 pr + 1].
     __device__ static void node_col(const KP &k, float *nodes) {
-        __shared__ cf lds[B * Lds<N1>::RS];
+        __shared__ cf lds[B * LdsC::RS];
         const int tid = threadIdx.x;
         int cbx, pr;
         xcd_block(cbx, pr);
@@ -1581,7 +1631,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>> {
             float a[4], b[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const cf z = lds[Lds<N1>::at(b4 + i, n1)];
+                const cf z = lds[LdsC::at(b4 + i, n1)];
                 a[i] = z.x * invN;
                 b[i] = z.y * invN;
             }
@@ -2358,6 +2408,15 @@ static int build_mask_table(KP &k, hipStream_t st, const float *mask_row, char *
     return PSS_OK;
 }
 
+// Extra LDS row pitch of the column kernels (tools/lds_banks.py): pass A's
+// spill-store loop reads 4 columns x 16 rows per 32-lane group (a 32/B pitch
+// offset spreads the columns over the 64 read banks); pass C's load loop
+// writes 4 columns x 4 rows per 16-lane group (16/B over the 32 write banks).
+constexpr int xrs_read(int B) { return B >= 32 ? 1 : 32 / B; }
+// (pass C measured 0.5 ms faster on the padded layout at C3: its transposes
+// gain nothing from the swizzle and the XOR addressing costs VALU)
+constexpr int xrs_write(int B) { return -1; }
+
 // Pair batches on two side streams (PSS_BATCHES > 1, fast path only): batch
 // b's pass A waits for batch b-1's pass A, so it runs next to batch b-1's
 // row pass (82 + 70 KB of LDS: both fit one CU) -- the compute-heavy
@@ -2445,8 +2504,8 @@ static int launch_batches(KP &k, hipStream_t st, int nb) {
 template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typename RF, typename RI,
           int TRF, int BC = B, int TC = T>
 static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
-    using PC = PairCols<N1, B, T, CF, CI>;
-    using PCC = PairCols<N1, BC, TC, CF, CI>;
+    using PC = PairCols<N1, B, T, CF, CI, xrs_read(B)>;
+    using PCC = PairCols<N1, BC, TC, CF, CI, xrs_write(BC)>;
     using PR = PairRows<N2, TR, RF, RI>;
     k.poff = k.p.chan0 & 1;
     k.npairs = (k.p.nchan + k.poff + 1) / 2;
@@ -2488,8 +2547,8 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
 template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typename RF, typename RI,
           int TRF, int BC, int TC>
 static int launch_pair_passes(KP &k, hipStream_t st) {
-    using PC = PairCols<N1, B, T, CF, CI>;
-    using PCC = PairCols<N1, BC, TC, CF, CI>;
+    using PC = PairCols<N1, B, T, CF, CI, xrs_read(B)>;
+    using PCC = PairCols<N1, BC, TC, CF, CI, xrs_write(BC)>;
     using PR = PairRows<N2, TR, RF, RI>;
     dim3 gc((unsigned)(N2 / B), (unsigned)k.npairs);
     tk_begin(TK_COLA, st);
@@ -2507,7 +2566,10 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     LAUNCHCHK();
     if (k.after_a) HIPCHK(hipEventRecord(k.after_a, st));   // batching: the next batch's pass A may start
     tk_begin(TK_ROW, st);
-    k_pair_row<PR, TR><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
+    if (k.p.tail_a)
+        k_pair_row<PR, TR, true><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
+    else
+        k_pair_row<PR, TR><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
     tk_end(st);
     LAUNCHCHK();
     const bool fast = PCC::kItemsExact && fast_epilogue(k);
@@ -2784,6 +2846,9 @@ static int validate(const PssPipeline *p) {
             return fail(PSS_EUNSUPPORTED, "N=%lld", (long long)p->nsamp);
         if (p->null_mode == PSS_NULL_DELAYED && fourstep_len(p->nsamp) && !p->mask_ramp)
             return fail(PSS_EINVAL, "delayed null needs mask_ramp");
+        if (p->tail_a && p->null_mode == PSS_NULL_DELAYED && !fourstep_len(p->nsamp))
+            return fail(PSS_EUNSUPPORTED, "scattering tail with a delayed null at N=%lld (the mask shares the "
+                        "filtered transform off the four-step lengths)", (long long)p->nsamp);
     }
     if (p->out_kind != PSS_OUT_NONE && !p->out) return fail(PSS_EINVAL, "out is NULL");
     return PSS_OK;

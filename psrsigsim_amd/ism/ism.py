@@ -41,6 +41,21 @@ def push_delay(signal, delays_ms):
     pend.shifts.append(delays_ms / signal._dt_ms())
 
 
+def push_tail(signal, a):
+    """Append a scattering-tail filter stage (ISM.scatter_broaden(tail=True)):
+    per channel decay factor a = exp(-dt/tau) of h[n] = (1 - a) a^n."""
+    if signal._ncols % 2:
+        raise ValueError("could not broadcast input array from shape (%d,) into shape (%d,)"
+                         % (signal._ncols - 1, signal._ncols))
+    pend = signal._pending
+    if pend is not None and (pend.null is not None or pend.noise is not None or pend.tail is not None):
+        signal._flush()
+        pend = None
+    if pend is None:
+        pend = signal._pend()
+    pend.tail = np.broadcast_to(np.asarray(a, dtype=np.float64), (signal.Nchan,)).copy()
+
+
 class ISM(object):
     """ism.py:12-358 (filterbank path)."""
 
@@ -96,15 +111,26 @@ class ISM(object):
         signal._FDshifted = True
 
     def scatter_broaden(self, signal, tau_d, ref_freq, beta=KOLMOGOROV_BETA, convolve=False,
-                        pulsar=None):
+                        pulsar=None, *, tail=False):
         """ism.py:158-240.  convolve=False: a pure extra delay
         tau_d (f/f_ref)^(-2 beta/(beta-2)); convolve=True: linear convolution
         of each channel's profile with a normalised exp(-t/tau) tail (before
-        make_pulses), replacing the pulsar's profile by a DataPortrait."""
+        make_pulses), replacing the pulsar's profile by a DataPortrait.
+
+        ``tail=True`` (keyword-only EXTENSION, no reference counterpart --
+        SURVEY.md App. A.11): scatter-broaden the time series itself -- every
+        channel's samples circularly convolved with the normalised exponential
+        (1 - a) a^n, a = exp(-dt / tau_c), tau_c scaled as above -- as the
+        transfer function H(k) = (1 - a)/(1 - a e^{-2 pi i k/N}) applied in the
+        same forward/inverse FFT pass as the delays (no extra HBM pass).  No
+        delay is added to ``signal.delay`` (the tail is a filter)."""
         f = signal._freqs_MHz()
         ref = float(to_value(make_quant(ref_freq, 'MHz'), 'MHz'))
         tau_ms = float(to_value(make_quant(tau_d, 's'), 's')) * 1e3
         tau_scaled = self.scale_tau_d(tau_ms, ref, f, beta=beta)
+        if tail:
+            push_tail(signal, np.exp(-signal._dt_ms() / np.asarray(tau_scaled, dtype=np.float64)))
+            return
         if not convolve:
             push_delay(signal, tau_scaled)
             return

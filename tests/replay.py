@@ -36,7 +36,10 @@ AMBIG_REL_TABLE = 2e-6
 # those at most TOL (as a fraction of all samples) may actually come out on
 # the other side of the threshold (FLIP_MAX_FRAC; both reported in STATS).
 AMBIG_MAX_FRAC = {"table": 2e-3, "packed": 3e-2}
-FLIP_MAX_FRAC = {"table": 1e-5, "packed": 1e-4}
+# fold mode (C4) boxes are chi2(Nfold ~ 1e4) values thresholded at 1: the
+# fp32 transform's ~2e-6 relative error (Bluestein) is ~0.02 absolute there,
+# so a few samples per 1e4 sit on the other side of the threshold
+FLIP_MAX_FRAC = {"table": 1e-5, "packed": 3e-4}
 
 
 def _prof():
