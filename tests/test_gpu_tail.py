@@ -76,7 +76,6 @@ def test_tail_fused_with_dispersion(N, hip_lib):
     ism = ISM()
     a = _a_of(sig, 1e-4, 1500.0)
     ism.scatter_broaden(sig, 1e-4, 1500.0, tail=True)
-    sig._dispersed_probe = None
     from psrsigsim_amd.ism.ism import push_delay
     delays_ms = np.linspace(3.0, 9.0, nchan)           # a delay stage in the same fused pass
     push_delay(sig, delays_ms)
