@@ -1273,7 +1273,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     // One wave per column (T = 64 B, N1/64 values per lane): the column FFTs
     // are wave-local (Fft<..., WAVE>: no workgroup barrier between stages);
     // only the transposes between sample-major items and columns need one.
-    using FW = Fft<(N1 % 64 == 0 ? N1 : 64), 1, 64, true>;     // (a placeholder when N1 % 64 != 0)
+    using FW = Fft<(N1 % 64 == 0 ? N1 : 64), 1, 64, true, XRS>;   // same row layout as LdsC (placeholder when N1 % 64 != 0)
     static constexpr bool kWaveCols = PSS_WAVE_COLS && (T == 64 * B) && (N1 % 64 == 0) && (N1 / 64 == E);
     static constexpr int RF0 = FF::template first<F...>();
     static constexpr int RFL = FF::template last_of<F...>();

@@ -92,6 +92,10 @@ def test_fast_path_bitwise_equals_generic(nchan, log2n, null, dm, hip_lib):
 
     L = _lib.lib()
     fast = run()
+    if log2n >= 22:
+        # run to run: a kernel reading LDS it did not write (stale from an
+        # earlier workgroup) shows up here even when both paths share it
+        np.testing.assert_array_equal(run(), fast)
     old = L.pss_set_flags(_lib.FLAG_NO_FAST)
     try:
         generic = run()
