@@ -15,7 +15,7 @@ import sys
 from collections import defaultdict
 
 KIND = {"k_pairA_fast": "fourstep_colA", "k_pairA": "fourstep_colA", "k_pair_row": "fourstep_row",
-        "k_pairC_fast": "fourstep_colC", "k_pairC": "fourstep_colC", "k_null_fix": "null_fix"}
+        "k_pairC_fast": "fourstep_colC", "k_pairC": "fourstep_colC", "k_null_fix": "null_fix", "k_null_fix_list": "null_fix"}
 
 
 def short(name):
