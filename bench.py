@@ -285,7 +285,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--nchan", type=int, default=NCHAN, help="channels per GPU")
     ap.add_argument("--log2n", type=int, default=LOG2N)
-    ap.add_argument("--cpu-chans", type=int, default=8, help="oracle sample size (channels)")
+    ap.add_argument("--cpu-chans", type=int, default=32, help="oracle sample size (channels; BASELINE.md §3: 32)")
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="all-core CPU baseline: concurrent single-threaded oracle processes (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
