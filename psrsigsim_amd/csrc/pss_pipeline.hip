@@ -37,6 +37,9 @@ static constexpr int kAbl = PSS_ABLATE;
 static constexpr bool kXcdMap = PSS_XCD_MAP != 0;
 static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 // fast pass C block width / threads for N = 2^22 (1024 x 4096 split)
+#ifndef PSS_ROW4K   // 2^17..2^21: rows of 4096 instead of 8192
+#define PSS_ROW4K 1
+#endif
 #ifndef PSS_BC
 #define PSS_BC 16
 #define PSS_TC 1024
@@ -2617,6 +2620,26 @@ static int run_fourstep(KP &k, hipStream_t st, const float *mask_row) {
         k.N2 = 8192;
         k.N1 = 2048;
         return launch_pair<2048, 4, 512, C2kF, C2kF, 8192, 1024, C8kF, C8kI, 512, 8, 1024>(k, st, mask_row);
+    }
+    if (PSS_ROW4K && N >= (1 << 17) && N <= (1 << 21)) {
+        // rows of 4096 (the C3 row kernel: two rows of a pair in 66 KB, two
+        // workgroups per CU) and N / 4096 columns; the column kernels keep
+        // their 8192 / N1-column blocks (N2 / B >= 16 blocks per pair)
+        k.N2 = 4096;
+        k.N1 = N / 4096;
+        switch (k.N1) {
+#define CASE4K(N1_, CF, CI)                                                                          \
+    case N1_:                                                                                        \
+        return launch_pair<N1_, 8192 / N1_, 512, CF, CF, 4096, 512, C4k, C4k, 256>(k, st, mask_row);
+            CASE4K(32, C32F, C32I)
+            CASE4K(64, C64F, C64I)
+            CASE4K(128, C128F, C128I)
+            CASE4K(256, C256, C256)
+            CASE4K(512, C512F, C512I)
+#undef CASE4K
+            default: break;
+        }
+        return fail(PSS_EUNSUPPORTED, "four-step: N=%lld", (long long)N);
     }
     if (N >= (1 << 17)) {
         k.N2 = 8192;
