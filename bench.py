@@ -67,12 +67,12 @@ ALG_BYTES = {"fourstep_colA": 4.0, "fourstep_row": 8.0, "fourstep_colC": 8.0, "n
              "single_pass": 4.0, "elementwise": 8.0, "fallback_dft": 28.0}
 
 
-def c3_step(pss, nchan_total, shard, nsamp_log2, ret_out=False):
+def c3_step(pss, nchan_total, shard, nsamp_log2, ret_out=False, plan_group=None):
     from psrsigsim_amd.signal import FilterBankSignal
     from psrsigsim_amd.pulsar import Pulsar, GaussProfile
     from psrsigsim_amd.ism import ISM
     from psrsigsim_amd.telescope import telescope as T
-    sig = FilterBankSignal(1400, 400, Nsubband=nchan_total, fold=False, shard=shard)
+    sig = FilterBankSignal(1400, 400, Nsubband=nchan_total, fold=False, shard=shard, plan_group=plan_group)
     psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
     ism = ISM()
     ism.scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
@@ -96,7 +96,7 @@ def b1855_profile():
     return _B1855["p"]
 
 
-def c4_step(pss, nchan_total, shard, gather):
+def c4_step(pss, nchan_total, shard, gather, plan_group=None):
     """BASELINE config C4: fold mode, 30 subints x 1024 bins over 30 min
     (30720 samples per channel: the mixed-radix 30 x 1024 four-step), DM 13.3,
     Arecibo radiometer noise; the folded filterbank is gathered to rank 0 over
@@ -110,7 +110,7 @@ def c4_step(pss, nchan_total, shard, gather):
     from psrsigsim_amd.ism import ISM
     from psrsigsim_amd.telescope import telescope as T
     sig = FilterBankSignal(1400, 400, Nsubband=nchan_total, sample_rate=F0_B1855 * 1024 * 1e-6, sublen=60.0,
-                           fold=True, shard=shard)
+                           fold=True, shard=shard, plan_group=plan_group)
     psr = Pulsar(1.0 / F0_B1855, 0.005, profiles=DataProfile(b1855_profile(), Nchan=nchan_total))
     psr.make_pulses(sig, tobs=1800.0)
     ISM().disperse(sig, 13.299393)
@@ -121,14 +121,14 @@ def c4_step(pss, nchan_total, shard, gather):
     return sig
 
 
-def c5_step(pss, nchan_total, shard, nsamp_log2):
+def c5_step(pss, nchan_total, shard, nsamp_log2, plan_group=None):
     """BASELINE config C5 per GPU: search mode, 2^24 samples, DM 500 (delays
     up to ~7x10^4 samples), Arecibo radiometer noise."""
     from psrsigsim_amd.signal import FilterBankSignal
     from psrsigsim_amd.pulsar import Pulsar, GaussProfile
     from psrsigsim_amd.ism import ISM
     from psrsigsim_amd.telescope import telescope as T
-    sig = FilterBankSignal(1400, 400, Nsubband=nchan_total, fold=False, shard=shard)
+    sig = FilterBankSignal(1400, 400, Nsubband=nchan_total, fold=False, shard=shard, plan_group=plan_group)
     psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
     psr.make_pulses(sig, tobs=(1 << nsamp_log2) * TOBS_PER_SAMPLE)
     ISM().disperse(sig, 500)
@@ -136,7 +136,7 @@ def c5_step(pss, nchan_total, shard, nsamp_log2):
     return sig
 
 
-def c2_step(pss, nchan_total, shard, nsamp_log2):
+def c2_step(pss, nchan_total, shard, nsamp_log2, plan_group=None):
     """BASELINE config C2: NANOGrav L-band search mode, 512 channels x 2^20
     samples at 20.48 us, J1713+0747 (P = 1/218.81 Hz from the par file, the
     reference's packaged 2048-bin DataProfile), disperse(DM = 15.917131),
@@ -146,7 +146,8 @@ def c2_step(pss, nchan_total, shard, nsamp_log2):
     from psrsigsim_amd.ism import ISM
     from psrsigsim_amd.telescope import telescope as T
     from psrsigsim_amd.data import j1713_profile
-    sig = FilterBankSignal(1500, 800, Nsubband=nchan_total, sample_rate=0.048828125, fold=False, shard=shard)
+    sig = FilterBankSignal(1500, 800, Nsubband=nchan_total, sample_rate=0.048828125, fold=False, shard=shard,
+                           plan_group=plan_group)
     psr = Pulsar(1.0 / 218.8118437960826270, 0.009, profiles=DataProfile(j1713_profile(), Nchan=nchan_total))
     psr.make_pulses(sig, tobs=(1 << nsamp_log2) * TOBS_PER_SAMPLE)
     ISM().disperse(sig, 15.917131)
@@ -166,13 +167,13 @@ WORKLOADS = {
 }
 
 
-def dry_step(pss, nchan_total, shard, nsamp_log2):
+def dry_step(pss, nchan_total, shard, nsamp_log2, plan_group=None):
     """--dry-run: the C3 calls up to the fused run's host plan (no device)."""
     from psrsigsim_amd.signal import FilterBankSignal
     from psrsigsim_amd.pulsar import Pulsar, GaussProfile
     from psrsigsim_amd.ism import ISM
     from psrsigsim_amd import _engine
-    sig = FilterBankSignal(1400, 400, Nsubband=nchan_total, fold=False, shard=shard)
+    sig = FilterBankSignal(1400, 400, Nsubband=nchan_total, fold=False, shard=shard, plan_group=plan_group)
     psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
     ism = ISM()
     ism.scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
@@ -289,6 +290,8 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="all-core CPU baseline: concurrent single-threaded oracle processes (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--whole-band-plan", action="store_true",
+                    help="N > 1: every rank plans the whole band's profile tables (no plan group)")
     ap.add_argument("--verbose", action="store_true", help="per-step wall times on stderr")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
                     help="BASELINE config (default: the north-star C3; c4/c5 are extra measurements)")
@@ -356,16 +359,23 @@ def main():
         with contextlib.redirect_stdout(sys.stderr):
             return _step()
 
+    # host planning of the profile tables split over the ranks (shard.RowSet):
+    # a gloo group next to the RCCL one, so the planning reductions stay on
+    # the host and never wait for the device
+    pg = None
+    if world > 1 and not args.whole_band_plan:
+        pg = dist.group.WORLD if args.dry_run else dist.new_group(backend="gloo")
+
     def _step():
         if args.dry_run:
-            return dry_step(pss, total, shard, args.log2n)
+            return dry_step(pss, total, shard, args.log2n, plan_group=pg)
         if args.workload == "c4":
-            return c4_step(pss, total, shard, gather=world > 1)
+            return c4_step(pss, total, shard, gather=world > 1, plan_group=pg)
         if args.workload == "c5":
-            return c5_step(pss, total, shard, args.log2n)
+            return c5_step(pss, total, shard, args.log2n, plan_group=pg)
         if args.workload == "c2":
-            return c2_step(pss, total, shard, args.log2n)
-        return c3_step(pss, total, shard, args.log2n)
+            return c2_step(pss, total, shard, args.log2n, plan_group=pg)
+        return c3_step(pss, total, shard, args.log2n, plan_group=pg)
 
     for _ in range(args.warmup):
         s = step()

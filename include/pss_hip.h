@@ -148,7 +148,10 @@ typedef struct PssPipeline {
                                1: PCHIP table, 2: analytic Gaussians, prof =
                                [nint][4] {peak, 1/width, amp/Amax, 0} and
                                knot_m = 1 (portraits.py:277-290)             */
-    int32_t reserved0;
+    int32_t prof_row0;      /* global channel of `prof`'s row 0 when the table
+                               holds a channel window (shard-local planning):
+                               channel c reads row c - prof_row0; 0 for a
+                               band-wide table (ignored when prof_rows == 1)  */
     const float *htab;      /* [nsamp/2 + 1] complex64 transfer function H(k)
                                of the reference's rfft bins (same for every
                                row): bin k gets H(k), bin N-k conj H(k), DC

@@ -172,9 +172,13 @@ class Source(object):
     a single shared row."""
 
     def __init__(self, mode, table, df, draw_norm, call_id, nph=0, M=0, nint=0,
-                 phase_step=0, inj=None):
+                 phase_step=0, inj=None, row_ids=None):
         self.mode = mode
         self.table = table            # np.float32, search [rows,nint,4] / fold [rows,nph]
+        # global channel of each table row when the table holds only this
+        # rank's channels (shard-local planning, shard.RowSet); None: row c is
+        # channel c (or one shared row)
+        self.row_ids = None if (row_ids is None or table.shape[0] == 1) else np.asarray(row_ids, dtype=np.int64)
         self.df = float(df)
         self.draw_norm = float(draw_norm)
         self.call_id = call_id
@@ -283,6 +287,15 @@ def build_pipeline(sig, pend, rows, chan0, data, out=None, ws_role="main"):
         if getattr(src, "dev_table", None) is None:
             src.dev_table = to_dev(src.table)
         p.prof = ptr(src.dev_table)
+        if src.row_ids is not None:
+            # a channel window: point at the row of global channel chan0
+            i = int(np.searchsorted(src.row_ids, chan0))
+            if not np.array_equal(src.row_ids[i:i + rows], np.arange(chan0, chan0 + rows)):
+                raise RuntimeError("profile table holds no rows for channels [%d, %d)" % (chan0, chan0 + rows))
+            p.prof = ctypes.c_void_p(src.dev_table.data_ptr() + i * src.dev_table[0].numel()
+                                     * src.dev_table.element_size())
+            p.prof_rows = src.table.shape[0] - i
+            p.prof_row0 = int(chan0)
     for name, arr in P["arrays"].items():
         t = u64_to_i64_tensor(arr) if name in ("ramp", "mask_ramp") else to_dev(arr)
         keep.append(t)

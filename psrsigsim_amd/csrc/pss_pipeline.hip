@@ -645,7 +645,7 @@ __device__ __forceinline__ void source4(const KP &k, int r, int64_t n0, int cnt,
                 Rng g(p.seed, p.call_gen, P_PULSE);
                 draw4(g, n0, c, p.gen_df, x);
             }
-            const int prow = (p.prof_rows == 1) ? 0 : (int)c;
+            const int prow = (p.prof_rows == 1) ? 0 : (int)c - p.prof_row0;
             if (p.src == PSS_SRC_SEARCH && p.gen_amp) {
                 // amplitude pulses: sqrt(calc_profiles(phase)) x N(0, 1)
 #pragma unroll
@@ -1303,7 +1303,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         const int64_t N2 = k.N2;
         const PssPipeline &p = k.p;
         const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
-        const int pra = (p.prof_rows == 1) ? 0 : (int)ca, prb = (p.prof_rows == 1) ? 0 : (int)cb;
+        const int pra = (p.prof_rows == 1) ? 0 : (int)ca - p.prof_row0, prb = (p.prof_rows == 1) ? 0 : (int)cb - p.prof_row0;
         const Rng g(p.seed, p.call_gen, P_PULSE);
         static_assert(!FAST || kItemsExact, "fast pass A: whole items per thread");
         if constexpr (FAST && !(kAbl & 1)) {
@@ -2852,6 +2852,11 @@ static int validate(const PssPipeline *p) {
         return fail(PSS_EINVAL, "search source needs a PCHIP table");
     if (p->src == PSS_SRC_FOLD && (!p->prof || p->nph < 1))
         return fail(PSS_EINVAL, "fold source needs a profile table");
+    if ((p->src == PSS_SRC_SEARCH || p->src == PSS_SRC_FOLD) && p->gen_amp != 2 && p->prof_rows != 1 &&
+        (p->prof_rows < 1 || p->prof_row0 < 0 || p->prof_row0 > p->chan0 ||
+         (int64_t)p->chan0 + p->nchan - p->prof_row0 > (int64_t)p->prof_rows))
+        return fail(PSS_EINVAL, "profile table rows [%d, %d) do not cover channels [%d, %d)", p->prof_row0,
+                    p->prof_row0 + p->prof_rows, p->chan0, p->chan0 + p->nchan);
     if (p->null_mode != PSS_NULL_NONE && (!p->null_rank || p->nph < 1))
         return fail(PSS_EINVAL, "null needs null_rank and nph");
     if (p->null_mode == PSS_NULL_DELAYED && !p->shift)

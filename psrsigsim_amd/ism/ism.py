@@ -137,10 +137,22 @@ class ISM(object):
         Nph = pulsar._nph(signal)
         pulsar.Profiles.init_profiles(Nph, signal.Nchan)
         full_profs = pulsar.Profiles.calc_profiles(np.linspace(0.0, 1.0, Nph), signal.Nchan)
-        full_profs = np.array(full_profs)      # convolved per channel (a uniform table no longer is)
         t = np.linspace(0, pulsar._P(), Nph)
-        tails = np.zeros((signal.Nchan, Nph))
         tau = np.atleast_1d(tau_scaled)
+        rs = getattr(signal, "_rowset", None)
+        if (rs is not None and tau.size == signal.Nchan and
+                (getattr(pulsar.Profiles, "_rowset", None) is rs or full_profs.shape[0] == signal.Nchan)):
+            # shard-local planning: convolve this rank's channels (+ the
+            # channel-0 pair) only; the portrait's band-wide max and max row
+            # are reductions over the plan group (shard.RowSet)
+            if getattr(pulsar.Profiles, "_rowset", None) is not rs:
+                full_profs = full_profs[rs.gids]
+            full_profs = np.array(full_profs)
+            tails = np.exp(-(t[None, :] * 1e3) / tau[rs.gids][:, None])
+            pulsar._Profiles = DataPortrait(self.convolve_profile(full_profs, tails, width=Nph), rowset=rs)
+            return
+        full_profs = np.array(full_profs)      # convolved per channel (a uniform table no longer is)
+        tails = np.zeros((signal.Nchan, Nph))
         tails[:tau.size, :] = np.exp(-(t[None, :] * 1e3) / tau[:, None])   # t [s] / tau [ms]
         pulsar._Profiles = DataPortrait(self.convolve_profile(full_profs, tails, width=Nph))
 

@@ -158,13 +158,27 @@ def ppoly_eval_np(x, c, ph):
 # ---------------------------------------------------------------------------
 # portraits
 # ---------------------------------------------------------------------------
-def _first_max_row(profiles):
+def _first_max_row(profiles, rowset=None):
     """``[pr for pr in profiles if pr.max() == 1.0][0]`` (portraits.py:45),
-    vectorised; IndexError when no row peaks at exactly 1.0, as there."""
+    vectorised; IndexError when no row peaks at exactly 1.0, as there.  With
+    a ``rowset`` (shard-local planning) ``profiles`` holds this rank's rows
+    and the first such row of the whole band comes from the rank holding it."""
+    if rowset is not None:
+        row = rowset.first_row(np.max(profiles, axis=1) == 1.0, profiles)
+        if row is None:
+            raise IndexError("list index out of range")
+        return row
     hit = np.flatnonzero(np.max(rows_of(profiles), axis=1) == 1.0)
     if hit.size == 0:
         raise IndexError("list index out of range")
     return rows_of(profiles)[hit[0]]
+
+
+def _band_max(profiles, rowset=None):
+    """table_max over the whole band (a reduction over the plan group when
+    ``profiles`` holds only this rank's rows)."""
+    m = table_max(profiles)
+    return m if rowset is None else rowset.max(m)
 
 
 class PulsePortrait(object):
@@ -178,13 +192,15 @@ class PulsePortrait(object):
             return self._profiles
         return self.calc_profiles(phases)
 
+    _rowset = None      # shard.RowSet: this portrait holds only the rank's rows
+
     def init_profiles(self, Nphase, Nchan=None):
         """portraits.py:32-45: sample at arange(N)/N, renormalise to max 1."""
         ph = np.arange(Nphase) / Nphase
         self._profiles = self.calc_profiles(ph, Nchan=Nchan)
-        self._Amax = table_max(self._profiles)
+        self._Amax = _band_max(self._profiles, self._rowset)
         self._profiles = like_rows(rows_of(self._profiles) / self.Amax, self._profiles)
-        self._max_profile = _first_max_row(self._profiles)
+        self._max_profile = _first_max_row(self._profiles, self._rowset)
 
     def calc_profiles(self, phases, Nchan=None):
         raise NotImplementedError()
@@ -282,7 +298,12 @@ class DataPortrait(PulsePortrait):
     enforced by appending the first column (phases arange(N+1)/N) when the
     first and last columns differ."""
 
-    def __init__(self, profiles, phases=None):
+    def __init__(self, profiles, phases=None, *, rowset=None):
+        """``rowset`` (keyword-only, shard-local planning): ``profiles`` holds
+        the rows of ``rowset.gids`` only; the portrait-wide decisions (the
+        periodic closure here, Amax and the max row later) are reductions over
+        its group."""
+        self._rowset = rowset
         profiles = np.asarray(profiles)
         uni = is_uniform(profiles)
         work = rows_of(profiles)            # a uniform table is processed as its one row
@@ -293,9 +314,12 @@ class DataPortrait(PulsePortrait):
                 work = np.where(neg, 0.0, work)
             else:
                 work[neg] = 0.0            # in place on the caller's array, as there
+        def band_any(flags):
+            f = bool(np.any(flags))
+            return f if rowset is None else rowset.any(f)
         if phases is None:
             N = work.shape[1]
-            if np.any(work[:, 0] != work[:, -1]):
+            if band_any(work[:, 0] != work[:, -1]):
                 work = np.append(work, work[:, 0][:, np.newaxis], axis=1)
                 phases = np.arange(N + 1) / N
             else:
@@ -305,7 +329,7 @@ class DataPortrait(PulsePortrait):
             if phases[-1] != 1:
                 phases = np.append(phases, 1)
                 work = np.append(work, work[:, 0][:, np.newaxis], axis=1)
-            elif np.any(work[:, 0] != work[:, -1]):
+            elif band_any(work[:, 0] != work[:, -1]):
                 if uni:
                     work = np.array(work)
                 work[:, -1] = work[:, 0]
@@ -331,8 +355,13 @@ class DataPortrait(PulsePortrait):
 
     def calc_profiles(self, phases, Nchan=None):
         profiles = self._generator(phases)
-        Amax = self.Amax if hasattr(self, '_Amax') else table_max(profiles)
+        Amax = self.Amax if hasattr(self, '_Amax') else _band_max(profiles, self._rowset)
         return like_rows(rows_of(profiles) / Amax, profiles)
+
+    def row_ids(self):
+        """Global channel of each row of this portrait's tables (None: row c is
+        channel c, or one shared row)."""
+        return None if self._rowset is None else self._rowset.gids
 
     # -- device export --------------------------------------------------
     def uniform_knots(self):

@@ -78,13 +78,22 @@ class Pulsar(object):
         Nph = self._nph(signal)
         self.Profiles.init_profiles(Nph, Nchan=signal.Nchan)
         full_profs = self.Profiles.calc_profiles(np.linspace(0.0, 1.0, Nph), Nchan=signal.Nchan)
+        rs = getattr(signal, "_rowset", None)
         if is_uniform(full_profs) and np.all(C == 1.0):
-            pass          # x 1.0 is the identity: the uniform table stays one row
+            rs = None     # x 1.0 is the identity: the uniform table stays one row
         else:
+            if rs is not None:
+                # shard-local planning: this rank's rows (and their factors)
+                if getattr(self.Profiles, "_rowset", None) is None and full_profs.shape[0] == signal.Nchan:
+                    full_profs = np.array(full_profs[rs.gids])
+                if full_profs.shape[0] == rs.gids.size:
+                    C = C[rs.gids]
+                else:
+                    rs = None
             if is_uniform(full_profs):
                 full_profs = np.array(full_profs)
             full_profs *= C   # in place: a 1-row portrait with Nchan > 1 raises, as there
-        self._Profiles = DataPortrait(full_profs)
+        self._Profiles = DataPortrait(full_profs, rowset=rs)
 
     def make_pulses(self, signal, tobs):
         """pulsar.py:107-151 (filterbank signals)."""
@@ -163,7 +172,7 @@ class Pulsar(object):
             signal._set_draw_norm(df=nfold)
             ncols = Nph * signal._nsub
             src = _engine.Source("fold", _dedupe(table).astype(np.float32), nfold,
-                                 signal._draw_norm, call, nph=Nph, inj=inj)
+                                 signal._draw_norm, call, nph=Nph, inj=inj, row_ids=_row_ids(self.Profiles))
         else:
             signal._sublen = self.period
             signal._nsub = int(np.round(tobs / P))
@@ -176,7 +185,7 @@ class Pulsar(object):
             inv = 1.0 / spp                           # cycles per sample
             step = int(round(math.ldexp(inv - math.floor(inv), 64)))
             src = _engine.Source("search", tab, 1.0, signal._draw_norm, call, M=M, nint=nint,
-                                 phase_step=step % (1 << 64), inj=inj)
+                                 phase_step=step % (1 << 64), inj=inj, row_ids=_row_ids(self.Profiles))
         signal._ncols = int(ncols)
         signal._pending = _engine.Pending(src)
         signal._row0 = None
@@ -239,6 +248,12 @@ class Pulsar(object):
         signal._flush()
         signal._pending = _engine.Pending(None)
         signal._pending.null = st
+
+
+def _row_ids(portrait):
+    """Global channels of a shard-local portrait's rows (None: band-wide)."""
+    f = getattr(portrait, "row_ids", None)
+    return f() if f is not None else None
 
 
 def _dedupe(tab):

@@ -6,7 +6,9 @@ executes any pending (deferred, fused) stages first.  The optional
 keyword-only ``shard=(c0, c1)`` keeps only global channels [c0, c1) on this
 process (multi-GPU channel sharding); every per-channel quantity and every
 random draw is keyed by the GLOBAL channel, so a sharded run produces exactly
-the rows of the unsharded one.
+the rows of the unsharded one.  Keyword-only ``plan_group`` (a host process
+group whose ranks hold a partition of the band) also splits the host
+planning of the profile tables over those ranks (psrsigsim_amd.shard.RowSet).
 """
 import numpy as np
 from scipy import stats
@@ -24,7 +26,7 @@ class FilterBankSignal(BaseSignal):
     _Nfold = None
 
     def __init__(self, fcent, bandwidth, Nsubband=512, sample_rate=None, sublen=None,
-                 dtype=np.float32, fold=True, *, shard=None):
+                 dtype=np.float32, fold=True, *, shard=None, plan_group=None):
         self._Npols = 1
         self._fcent = make_quant(fcent, 'MHz')
         if bandwidth < 0:
@@ -58,6 +60,12 @@ class FilterBankSignal(BaseSignal):
         if not (0 <= c0 < c1 <= Nsubband):
             raise ValueError("bad shard %r for %d channels" % (shard, Nsubband))
         self._c0, self._c1 = c0, c1
+        # shard-local host planning (shard.RowSet): the ranks of plan_group
+        # hold a partition of the band and plan their own profile rows
+        self._rowset = None
+        if plan_group is not None:
+            from ..shard import RowSet
+            self._rowset = RowSet(c0, c1, Nsubband, plan_group)
         self._buf = None
         self._row0 = None
         self._track_row0 = True

@@ -21,15 +21,15 @@ def _free_port():
     return p
 
 
-def _plan(nchan, shard):
+def _plan(nchan, shard, plan_group=None, specidx=0.0, ret_psr=False):
     import psrsigsim_amd as pss
     from psrsigsim_amd.signal import FilterBankSignal
     from psrsigsim_amd.pulsar import Pulsar, GaussProfile
     from psrsigsim_amd.ism import ISM
     from psrsigsim_amd import _engine
     pss.seed(99)
-    sig = FilterBankSignal(1400, 400, Nsubband=nchan, fold=False, shard=shard)
-    psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
+    sig = FilterBankSignal(1400, 400, Nsubband=nchan, fold=False, shard=shard, plan_group=plan_group)
+    psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1), specidx=specidx, ref_freq=1300)
     ism = ISM()
     ism.scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
     psr.make_pulses(sig, tobs=(1 << 16) * 20.48e-6)
@@ -37,7 +37,58 @@ def _plan(nchan, shard):
     ism.FD_shift(sig, [1e-4, 2e-5])
     c0, c1 = sig.shard
     P = _engine.plan_pipeline(sig, sig._pending, c1 - c0, c0)
+    if ret_psr:
+        return sig, P, psr
     return sig, P
+
+
+def _plan_group_worker(rank, world, port, nchan, q):
+    """Shard-local planning (plan_group): each rank's profile tables hold
+    only its channels + the channel-0 pair, bitwise the rows of the
+    whole-band plan, and the band-wide scalars match."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from psrsigsim_amd.shard import channel_block
+    c0, c1 = channel_block(nchan, rank, world)
+    ok = True
+    for specidx in (0.0, -1.6):
+        sig, P, psr = _plan(nchan, (c0, c1), plan_group=dist.group.WORLD, specidx=specidx, ret_psr=True)
+        fsig, F, fpsr = _plan(nchan, None, specidx=specidx, ret_psr=True)
+        src, fsrc = sig._pending.source, fsig._pending.source
+        ids = src.row_ids
+        want = sorted(set([0, 1]) | set(range(c0, c1)))
+        ok &= ids is not None and list(ids) == want
+        ok &= src.table.shape[0] == len(want)
+        ok &= np.array_equal(src.table, fsrc.table[want])
+        ok &= float(sig._Smax.value) == float(fsig._Smax.value)
+        ok &= psr.Profiles.Amax == fpsr.Profiles.Amax
+        ok &= np.array_equal(psr.Profiles._max_profile, fpsr.Profiles._max_profile)
+        ok &= np.array_equal(psr.Profiles._calcOffpulseWindow(Nphase=244),
+                             fpsr.Profiles._calcOffpulseWindow(Nphase=244))
+        for k in ("ramp", "nyq_re", "nyq_im"):
+            ok &= np.array_equal(P["arrays"][k], F["arrays"][k][c0:c1])
+        for k in ("seed", "call_gen", "phase_step", "knot_m", "nint", "draw_norm", "src"):
+            ok &= P[k] == F[k]
+    flag = torch.tensor([1 if ok else 0])
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        q.put(int(flag.item()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,nchan", [(2, 16), (3, 10)])
+def test_shard_local_planning_gloo(world, nchan):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plan_group_worker, args=(r, world, port, nchan, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) == 1
 
 
 def _worker(rank, world, port, nchan, q):
