@@ -40,6 +40,9 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 #ifndef PSS_ROW4K   // 2^17..2^21: rows of 4096 instead of 8192
 #define PSS_ROW4K 1
 #endif
+#ifndef PSS_MASK_SIDE   // build the delayed-null mask table on a side stream next to pass A
+#define PSS_MASK_SIDE 1
+#endif
 #ifndef PSS_BC
 #define PSS_BC 16
 #define PSS_TC 1024
@@ -154,6 +157,7 @@ struct KP {
     int mbB;                // column-block width B of pass C (mbits layout)
     const cf *rtab;         // [nchan][RFL] row-pass ramp factors (k_ramp_tab)
     hipEvent_t after_a;     // batching: recorded after this launch's pass A (or NULL)
+    hipEvent_t mask_ready;  // mask table built on a side stream: wait before its first use (or NULL)
     const uint32_t *wlist;  // delayed null: table words with a nulled position (any f)
     const uint32_t *nwlist; // its length (device)
 };
@@ -2519,8 +2523,23 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
         // the mask table's position arithmetic is for N = 2^m (validate()
         // sends delayed nulls of other lengths to the direct path)
         if constexpr ((N1 & (N1 - 1)) == 0) {
-            const int rc = build_mask_table<N1, B, T, CF, CI, N2, TR, RF, RI, TRF>(k, st, mask_row, w, L);
+            // With the data in the FFT and the fast passes, nothing reads the
+            // table before the null fix-up: build it on a side stream next to
+            // pass A (its dozen small launches then cost no time on the main
+            // stream); the fix-up waits for it.
+            SideStreams *ss = (PSS_MASK_SIDE && k.p.data_in_fft && g_batches <= 1) ? side_streams() : nullptr;
+            hipStream_t ms = st;
+            if (ss) {
+                HIPCHK(hipEventRecord(ss->ev[30], st));
+                HIPCHK(hipStreamWaitEvent(ss->s[0], ss->ev[30], 0));
+                ms = ss->s[0];
+            }
+            const int rc = build_mask_table<N1, B, T, CF, CI, N2, TR, RF, RI, TRF>(k, ms, mask_row, w, L);
             if (rc) return rc;
+            if (ss) {
+                HIPCHK(hipEventRecord(ss->ev[31], ms));
+                k.mask_ready = ss->ev[31];
+            }
         } else {
             return fail(PSS_EUNSUPPORTED, "delayed null on the mixed-radix four-step (N=%lld)", (long long)k.N);
         }
@@ -2576,6 +2595,7 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     tk_end(st);
     LAUNCHCHK();
     const bool fast = PCC::kItemsExact && fast_epilogue(k);
+    if (k.mask_ready && !fast) HIPCHK(hipStreamWaitEvent(st, k.mask_ready, 0));   // generic pass C reads the bits
     tk_begin(TK_COLC, st);
     if (fast) {
         if constexpr (PCC::kItemsExact)
@@ -2586,6 +2606,7 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     tk_end(st);
     LAUNCHCHK();
     if (fast && k.mtab) {
+        if (k.mask_ready) HIPCHK(hipStreamWaitEvent(st, k.mask_ready, 0));
         tk_begin(TK_NULLFIX, st);
         if (PSS_NULL_LIST) {
             // grid-stride over the word list: ~1/8 of the words per channel
