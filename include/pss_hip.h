@@ -168,6 +168,13 @@ typedef struct PssPipeline {
                                i.e. bin k x H(k) = (1-a) / (1 - a e^{-2 pi i k/N})
                                in the same forward/inverse pass as the delay
                                ramp; NULL = none                             */
+    int32_t prof_split;     /* SEARCH: 1 = `prof` holds split cells for a portrait
+                               on non-uniform phases: [prof_rows][nint][8]
+                               (the cubics left and right of the cell's one
+                               interior knot, in the cell coordinate u) followed
+                               by [nint] split points (u >= split: right cubic;
+                               2 = no knot in the cell); knot_m = nint cells */
+    int32_t reserved1;
 } PssPipeline;
 
 /* Library / device info. */

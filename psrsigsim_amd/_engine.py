@@ -172,13 +172,16 @@ class Source(object):
     a single shared row."""
 
     def __init__(self, mode, table, df, draw_norm, call_id, nph=0, M=0, nint=0,
-                 phase_step=0, inj=None, row_ids=None):
+                 phase_step=0, inj=None, row_ids=None, split=None):
         self.mode = mode
         self.table = table            # np.float32, search [rows,nint,4] / fold [rows,nph]
         # global channel of each table row when the table holds only this
         # rank's channels (shard-local planning, shard.RowSet); None: row c is
         # channel c (or one shared row)
         self.row_ids = None if (row_ids is None or table.shape[0] == 1) else np.asarray(row_ids, dtype=np.int64)
+        # non-uniform portrait phases: [M] split points after the [rows, M, 8]
+        # split-cell table (PssPipeline.prof_split)
+        self.split = split
         self.df = float(df)
         self.draw_norm = float(draw_norm)
         self.call_id = call_id
@@ -220,7 +223,8 @@ def plan_pipeline(sig, pend, rows, chan0):
                  prof_rows=src.table.shape[0], nint=src.nint, nph=src.nph,
                  phase_step=src.phase_step, knot_m=src.M, gen_df=src.df,
                  draw_norm=src.draw_norm, call_gen=src.call_id,
-                 gen_amp=(2 if src.amp == "gauss" else 1) if src.amp else 0)
+                 gen_amp=(2 if src.amp == "gauss" else 1) if src.amp else 0,
+                 prof_split=1 if getattr(src, "split", None) is not None else 0)
         if src.inj is not None:
             A["inj_gen"] = inj_rows(src.inj, gidx)
     nul = pend.null
@@ -285,15 +289,17 @@ def build_pipeline(sig, pend, rows, chan0, data, out=None, ws_role="main"):
         # rows are indexed by GLOBAL channel inside the kernel (or row 0 when
         # the table is shared); the device copy is cached on the stage.
         if getattr(src, "dev_table", None) is None:
-            src.dev_table = to_dev(src.table)
+            flat = np.ascontiguousarray(src.table, dtype=np.float32).ravel()
+            if getattr(src, "split", None) is not None:
+                flat = np.concatenate([flat, np.asarray(src.split, dtype=np.float32)])
+            src.dev_table = to_dev(flat)
         p.prof = ptr(src.dev_table)
         if src.row_ids is not None:
             # a channel window: point at the row of global channel chan0
             i = int(np.searchsorted(src.row_ids, chan0))
             if not np.array_equal(src.row_ids[i:i + rows], np.arange(chan0, chan0 + rows)):
                 raise RuntimeError("profile table holds no rows for channels [%d, %d)" % (chan0, chan0 + rows))
-            p.prof = ctypes.c_void_p(src.dev_table.data_ptr() + i * src.dev_table[0].numel()
-                                     * src.dev_table.element_size())
+            p.prof = ctypes.c_void_p(src.dev_table.data_ptr() + i * int(src.table[0].size) * 4)
             p.prof_rows = src.table.shape[0] - i
             p.prof_row0 = int(chan0)
     for name, arr in P["arrays"].items():

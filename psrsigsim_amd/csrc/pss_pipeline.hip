@@ -591,7 +591,16 @@ __device__ __forceinline__ void phase_delta(const PssPipeline &p, uint32_t &dlo,
 }
 
 __device__ __forceinline__ float pchip_row(const KP &k, int prow, uint32_t iv, float u) {
-    const float4 cc = reinterpret_cast<const float4 *>(k.p.prof)[(int64_t)prow * k.p.nint + iv];
+    float4 cc;
+    if (k.p.prof_split) {
+        // non-uniform knots: cell iv holds the cubics on either side of its
+        // one interior knot (both in the cell coordinate u)
+        const float4 *c = reinterpret_cast<const float4 *>(k.p.prof) + ((int64_t)prow * k.p.nint + iv) * 2;
+        const float s = k.p.prof[(int64_t)k.p.prof_rows * k.p.nint * 8 + iv];
+        cc = (u >= s) ? c[1] : c[0];
+    } else {
+        cc = reinterpret_cast<const float4 *>(k.p.prof)[(int64_t)prow * k.p.nint + iv];
+    }
     return fmaf(fmaf(fmaf(cc.x, u, cc.y), u, cc.z), u, cc.w);
 }
 
@@ -2324,7 +2333,7 @@ static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
 static bool fast_source(const PssPipeline &p) {
     if (g_flags & PSS_FLAG_NO_FAST) return false;
     return p.src == PSS_SRC_SEARCH && !p.gen_amp && p.gen_df == 1.0f && !p.inj_gen && p.null_mode != PSS_NULL_UNDELAYED &&
-           p.nint <= kFastNint;
+           p.nint <= kFastNint && !p.prof_split;
 }
 static bool fast_epilogue(const KP &k) {
     const PssPipeline &p = k.p;
@@ -2873,6 +2882,8 @@ static int validate(const PssPipeline *p) {
         return fail(PSS_EINVAL, "search source needs a PCHIP table");
     if (p->src == PSS_SRC_FOLD && (!p->prof || p->nph < 1))
         return fail(PSS_EINVAL, "fold source needs a profile table");
+    if (p->prof_split && (p->src != PSS_SRC_SEARCH || p->gen_amp == 2 || p->knot_m != (uint32_t)p->nint))
+        return fail(PSS_EINVAL, "split-cell profile tables are for the PCHIP search source with knot_m == nint");
     if ((p->src == PSS_SRC_SEARCH || p->src == PSS_SRC_FOLD) && p->gen_amp != 2 && p->prof_rows != 1 &&
         (p->prof_rows < 1 || p->prof_row0 < 0 || p->prof_row0 > p->chan0 ||
          (int64_t)p->chan0 + p->nchan - p->prof_row0 > (int64_t)p->prof_rows))

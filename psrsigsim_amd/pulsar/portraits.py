@@ -376,16 +376,65 @@ class DataPortrait(PulsePortrait):
     def device_table(self):
         """float32 [rows, nint, 4] coefficients in the local coordinate
         u = (phase - k/M) * M, ordered (u^3, u^2, u^1, u^0), divided by Amax
-        so the device evaluates calc_profiles directly; plus (M, nint)."""
+        so the device evaluates calc_profiles directly; plus (M, nint).  On
+        non-uniform knots see :meth:`split_table` (the third element is then
+        the [M] split points instead of nint, and the table is [rows, M, 8])."""
         geo = self.uniform_knots()
         if geo is None:
-            raise NotImplementedError("non-uniform portrait phases on the device path")
+            return self.split_table()
         M, nint = geo
         h = 1.0 / M
         amax = self.Amax if hasattr(self, '_Amax') else 1.0
         # = (self._coef * [h**3, h**2, h, 1] / amax).astype(float32), natively
         # (one row for a uniform table: the device then shares it)
         return _lib.host_device_table(np.ascontiguousarray(rows_of(self._coef)), h, amax), M, nint
+
+
+    def split_table(self, max_cells=1 << 16):
+        """Device form of a portrait on NON-uniform phases: M = 2^m uniform
+        cells over [0, 1), each holding at most one interior breakpoint; per
+        cell and row the cubic in force at the cell's start and the one after
+        its breakpoint, both re-expanded in the cell coordinate u = phase M - c
+        (float64, then /Amax to float32), and the breakpoint's u (2 when the
+        cell has none).  Evaluating the cubic on the breakpoint's side is the
+        piecewise polynomial the reference evaluates (interval = last
+        breakpoint <= phase, end pieces extrapolated; portraits.py:252).
+        Returns (table [rows, M, 8] float32, M, split [M] float32)."""
+        x = self._knots
+        K = x.size - 1
+        c = np.asarray(rows_of(self._coef), dtype=np.float64)          # [rows, K, 4], powers 3..0
+        inner = x[1:K]                       # breakpoints where the piece changes
+        M = 1
+        while M < 2 * K:
+            M *= 2
+        while True:
+            pos = inner * M
+            cell = np.floor(pos).astype(np.int64)
+            strict = pos != cell            # on a cell boundary: no split needed
+            if cell[strict].size == np.unique(cell[strict]).size:
+                break
+            M *= 2
+            if M > max_cells:
+                raise NotImplementedError("portrait breakpoints closer than 1/%d of a period" % max_cells)
+        starts = np.arange(M, dtype=np.float64) / M
+        iL = np.clip(np.searchsorted(x, starts, side="right") - 1, 0, K - 1)
+        split = np.full(M, 2.0)
+        iR = iL.copy()
+        sc = cell[strict]
+        split[sc] = pos[strict] - sc
+        iR[sc] = np.clip(np.searchsorted(x, inner[strict], side="right") - 1, 0, K - 1)
+        h = 1.0 / M
+
+        def expand(idx):
+            d = starts - x[idx]                                       # [M]
+            ci = c[:, idx, :]                                         # [rows, M, 4]
+            c3, c2, c1, c0 = ci[..., 0], ci[..., 1], ci[..., 2], ci[..., 3]
+            return np.stack([c3 * h ** 3, (3 * c3 * d + c2) * h ** 2, ((3 * c3 * d + 2 * c2) * d + c1) * h,
+                             ((c3 * d + c2) * d + c1) * d + c0], axis=-1)
+        amax = self.Amax if hasattr(self, '_Amax') else 1.0
+        tab = np.concatenate([expand(iL), expand(iR)], axis=-1) / amax
+        tab = like_rows(tab, self._coef) if tab.shape[0] == 1 else tab
+        return np.ascontiguousarray(rows_of(tab)).astype(np.float32), M, split.astype(np.float32)
 
 
 class UserPortrait(PulsePortrait):

@@ -140,9 +140,9 @@ class Pulsar(object):
                                  nint=len(pk), phase_step=step % (1 << 64), inj=inj)
             src.amp = "gauss"
         elif hasattr(prof, "device_table"):
-            tab, M, nint = prof.device_table()
+            tab, M, nint, split = _device_table(prof)
             src = _engine.Source("search", _dedupe(tab), 1.0, 1.0, call, M=M, nint=nint,
-                                 phase_step=step % (1 << 64), inj=inj)
+                                 phase_step=step % (1 << 64), inj=inj, split=split)
             src.amp = "pchip"
         else:
             raise NotImplementedError("amplitude pulses from a %s" % type(prof).__name__)
@@ -179,13 +179,14 @@ class Pulsar(object):
             signal._set_draw_norm(df=1)
             signal._nsamp = int((tobs * sr) * 1e6)
             ncols = signal._nsamp
-            tab, M, nint = self.Profiles.device_table()
+            tab, M, nint, split = _device_table(self.Profiles)
             tab = _dedupe(tab)
             spp = (sr * P) * 1e6                      # samples per period
             inv = 1.0 / spp                           # cycles per sample
             step = int(round(math.ldexp(inv - math.floor(inv), 64)))
             src = _engine.Source("search", tab, 1.0, signal._draw_norm, call, M=M, nint=nint,
-                                 phase_step=step % (1 << 64), inj=inj, row_ids=_row_ids(self.Profiles))
+                                 phase_step=step % (1 << 64), inj=inj, row_ids=_row_ids(self.Profiles),
+                                 split=split)
         signal._ncols = int(ncols)
         signal._pending = _engine.Pending(src)
         signal._row0 = None
@@ -248,6 +249,15 @@ class Pulsar(object):
         signal._flush()
         signal._pending = _engine.Pending(None)
         signal._pending.null = st
+
+
+def _device_table(portrait):
+    """(table, M, nint, split): uniform knots -> split None; non-uniform
+    knots -> the split-cell table (DataPortrait.split_table), nint = M."""
+    tab, M, third = portrait.device_table()
+    if np.ndim(third) == 1:
+        return tab, M, M, np.asarray(third, dtype=np.float32)
+    return tab, M, third, None
 
 
 def _row_ids(portrait):

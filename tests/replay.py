@@ -95,10 +95,21 @@ def b1855():
     return template_profile(B1855_TEMPLATE)
 
 
+def nonuniform_portrait(nchan, n=96):
+    """A 1-D Gaussian sampled on NON-uniform phases (u^1.3 of a uniform grid),
+    tiled over ``nchan`` rows: (values [nchan, n], phases [n])."""
+    ph = (np.arange(n) / n) ** 1.3
+    prof = np.exp(-0.5 * ((ph - 0.45) / 0.04) ** 2) + 0.3 * np.exp(-0.5 * ((ph - 0.6) / 0.02) ** 2)
+    return np.tile(prof, (nchan, 1)), ph
+
+
 def _oracle_profile(spec):
     kind = spec[0]
     if kind == "b1855":
         return O.DataProfile(b1855(), nchan=spec[1])
+    if kind == "dataph":
+        vals, ph = nonuniform_portrait(spec[1])
+        return O.DataPortrait(vals, phases=ph)
     if kind == "gauss":
         return O.GaussPortrait(*spec[1:])
     if kind == "gaussarr":
@@ -256,6 +267,10 @@ def run_case(name, fused=True, case=None, seed=None):
         prof = GaussProfile(np.array([0.3, 0.6]), np.array([0.02, 0.05]), np.array([0.5, 1.0]))
     elif spec[0] == "b1855":
         prof = DataProfile(b1855(), Nchan=spec[1])
+    elif spec[0] == "dataph":
+        from psrsigsim_amd.pulsar.portraits import DataPortrait
+        vals, ph = nonuniform_portrait(spec[1])
+        prof = DataPortrait(vals, phases=ph)
     else:
         prof = DataProfile(_prof(), Nchan=spec[1])
     psr = Pulsar(ps["period"], ps["Smean"], profiles=prof, specidx=ps.get("specidx", 0.0),

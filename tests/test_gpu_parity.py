@@ -151,6 +151,23 @@ def test_c4_fold_mixed_radix_vs_oracle(nchan, null, template, hip_lib):
     assert not bad, errs
 
 
+@pytest.mark.parametrize("log2n,null", [(12, False), (16, True), (22, False)])
+def test_nonuniform_portrait_phases_vs_oracle(log2n, null, hip_lib):
+    """A DataPortrait on NON-uniform phases (split-cell device table,
+    PssPipeline.prof_split; the reference's PchipInterpolator over those
+    knots) through pulses, dispersion, (delayed null) and noise, against the
+    oracle with injected draws: single pass (2^12), four-step pair path."""
+    ops = [("make_pulses", (1 << log2n) * 20.48e-6, "pulses"), ("disperse", 100, "disperse")]
+    if null:
+        ops.append(("null", 0.1, "null"))
+    ops.append(("observe", "Arecibo", "Lband_PUPPI", True, "noise"))
+    case = dict(sig=dict(fcent=1400, bw=400, nchan=3, fold=False),
+                psr=dict(period=0.005, Smean=1.0, prof=("dataph", 3)), ops=ops)
+    errs = replay.run_case(None, fused=True, case=case, seed=log2n + 7)
+    bad = {k: v for k, v in errs.items() if not v <= TOL}
+    assert not bad, errs
+
+
 @pytest.mark.parametrize("fused", [True, False], ids=["fused", "staged"])
 @pytest.mark.parametrize("N,nchan,null", [(10006, 3, True), (100002, 2, True), (100002, 3, False)])
 def test_bluestein_pipeline_vs_oracle(N, nchan, null, fused, hip_lib):
