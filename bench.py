@@ -255,6 +255,21 @@ def cpu_model():
     return platform.processor()
 
 
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """fd-level redirect of stdout to stderr: gloo's C++ layer prints its
+    connection messages on stdout, which must carry only the JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def _free_port():
     import socket
     so = socket.socket()
@@ -290,6 +305,10 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="all-core CPU baseline: concurrent single-threaded oracle processes (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="N > 1 process group (nccl = RCCL over xGMI; gloo only to rehearse on one GPU)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a one-GPU box: every rank on cuda:0 (with --backend gloo)")
     ap.add_argument("--whole-band-plan", action="store_true",
                     help="N > 1: every rank plans the whole band's profile tables (no plan group)")
     ap.add_argument("--verbose", action="store_true", help="per-step wall times on stderr")
@@ -322,10 +341,18 @@ def main():
               file=sys.stderr)
     if args.dry_run:
         if world > 1:
-            dist.init_process_group("gloo")
+            with _stdout_to_stderr():
+                dist.init_process_group("gloo")
+                dist.barrier()
     elif world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = 0 if args.same_device else local
+        torch.cuda.set_device(dev)
+        with _stdout_to_stderr():
+            if args.backend == "gloo":
+                dist.init_process_group("gloo")
+                dist.barrier()
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     ranks = dist.get_world_size() if world > 1 else 1
     import psrsigsim_amd as pss
     from psrsigsim_amd import _lib
@@ -364,7 +391,12 @@ def main():
     # the host and never wait for the device
     pg = None
     if world > 1 and not args.whole_band_plan:
-        pg = dist.group.WORLD if args.dry_run else dist.new_group(backend="gloo")
+        if args.dry_run or args.backend == "gloo":
+            pg = dist.group.WORLD
+        else:
+            with _stdout_to_stderr():
+                pg = dist.new_group(backend="gloo")
+                dist.barrier(group=pg)
 
     def _step():
         if args.dry_run:
@@ -407,7 +439,8 @@ def main():
         launches = _lib.timing_collect()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], device="cpu" if args.dry_run else "cuda", dtype=torch.float64)
+        t = torch.tensor([elapsed], device="cpu" if (args.dry_run or args.backend == "gloo") else "cuda",
+                         dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     per_step = elapsed / args.steps

@@ -199,8 +199,8 @@ def test_bench_self_launch_world2():
                             "--warmup", "0", "--dry-run", "--log2n", "14", "--nchan", "8", "--scaling", scaling],
                            capture_output=True, text=True, timeout=300, cwd=root)
         assert r.returncode == 0, r.stderr[-2000:]
-        lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-        assert len(lines) == 1, r.stdout
+        lines = [l for l in r.stdout.splitlines() if l.strip()]
+        assert len(lines) == 1 and lines[0].startswith("{"), r.stdout   # stdout carries only the JSON line
         line = json.loads(lines[0])
         assert line["n_gpus"] == 2 and line["ranks"] == 2
         assert line["scaling"] == scaling
