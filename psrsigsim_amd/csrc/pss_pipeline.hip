@@ -67,6 +67,27 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 #ifndef PSS_SPILL_AUX
 #define PSS_SPILL_AUX 0
 #endif
+// Pair spill layout.  1: the two rows {k1, N1 - k1} ({0, N1/2}) that one
+// row-pass workgroup transforms together are interleaved sample by sample,
+// complex index (p N2 + n2) 2 + side (il_row below): pass A writes, and pass
+// C reads, one contiguous segment of 2 B complex per row pair instead of B
+// per row, and the row pass reads one contiguous block.  0: row-major
+// [k1][n2] (experiment switch).
+#ifndef PSS_PAIR_IL
+#define PSS_PAIR_IL 0
+#endif
+static constexpr bool kPairIL = PSS_PAIR_IL != 0;
+// row k1 of side `side` of interleaved row pair p
+__device__ __forceinline__ int il_row(int p, int side, int N1) {
+    return side == 0 ? p : (p == 0 ? N1 / 2 : N1 - p);
+}
+// Padding of each pair-spill row (complex) on the power-of-two split: the
+// rows' starts then do not all fall on the same HBM channel (experiment
+// switch; the mixed-radix split shares fallback bytes and keeps no pad).
+#ifndef PSS_SPILL_PAD
+#define PSS_SPILL_PAD 0
+#endif
+static constexpr int kSpillPad = PSS_SPILL_PAD;
 // fast pass C block width / threads for N = 2^22 on the 512 x 8192 split
 #ifndef PSS_BC8
 #define PSS_BC8 16
@@ -144,7 +165,8 @@ struct KP {
     // four-step pair mode (two channels per complex row)
     int npairs;
     int poff;       // chan0 & 1: pairs are (even, odd) GLOBAL channels
-    cf *Yd;         // data pair spill    [npairs][N1][N2]
+    int64_t sp;     // pair spill row pitch (complex; 0 = N2): N2 + PSS_SPILL_PAD on the 2^m split
+    cf *Yd;         // data pair spill    [npairs][N1][sp]
     cf *Ym;         // node pair spill    [KCH/2][N1][N2] (mask table build)
     const cf *Mspec;// mask spectrum      [N1][N2] (natural k2 per row k1)
     // delayed-null mask table (four-step lengths; see k_mask_table)
@@ -161,6 +183,10 @@ struct KP {
     const uint32_t *wlist;  // delayed null: table words with a nulled position (any f)
     const uint32_t *nwlist; // its length (device)
 };
+// pair spill row pitch and per-pair stride (complex)
+__host__ __device__ __forceinline__ int64_t rpitch(const KP &k) { return k.sp ? k.sp : k.N2; }
+__host__ __device__ __forceinline__ int64_t pstride(const KP &k) { return k.N1 * rpitch(k); }
+
 
 // ---------------------------------------------------------------------------
 // Delayed-null mask table.
@@ -1144,6 +1170,13 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
     static_assert(RIL == RF0, "inverse plan must be the reversed forward plan");
     static constexpr int LR = N2 / RF0;
     static constexpr int LRL = N2 / RFL;
+    // byte offset of (row, n2) in a pair spill (PSS_PAIR_IL: side b of row
+    // pair p), and the offset step of the q-th first-stage input (n2 + q LR)
+    static constexpr uint32_t kQS = (kPairIL ? 16u : 8u) * (uint32_t)LR;
+    __device__ static __forceinline__ uint32_t spill_off(uint32_t RP, int p, int row, int b, int n2) {
+        return kPairIL ? (((uint32_t)p * RP + (uint32_t)n2) * 2u + (uint32_t)b) * 8u
+                       : ((uint32_t)row * RP + (uint32_t)n2) * 8u;
+    }
 
     // MASK = false: data pair of channels (2pr - poff, 2pr + 1 - poff).
     // MASK = true : node pair (2pr, 2pr + 1) of the mask table build -- the
@@ -1165,15 +1198,16 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
         const uint64_t sta = (uint64_t)(k.N / RFL) * rwa, stb = (uint64_t)(k.N / RFL) * rwb;
         const uint64_t nwa = (uint64_t)k.N * rwa, nwb = (uint64_t)k.N * rwb;
         cf v[E];
-        const uint32_t pbytes = (uint32_t)(k.N * 8);
+        const uint32_t pbytes = (uint32_t)(pstride(k) * 8);
+        const uint32_t RP = (uint32_t)rpitch(k);
         if (data) {
-            const Buf Y(k.Yd + (int64_t)pr * k.N, pbytes);
+            const Buf Y(k.Yd + (int64_t)pr * pstride(k), pbytes);
 #pragma unroll
             for (int ib = 0; ib < E / RF0; ++ib) {
                 const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
-                const uint32_t off = (uint32_t)((b ? rowB : rowA) * N2 + jj) * 8u;
+                const uint32_t off = spill_off(RP, j, b ? rowB : rowA, b, jj);
 #pragma unroll
-                for (int q = 0; q < RF0; ++q) v[ib * RF0 + q] = Y.ld2(off, q * LR * 8);
+                for (int q = 0; q < RF0; ++q) v[ib * RF0 + q] = Y.ld2(off, q * kQS);
             }
             if constexpr (!(kAbl & 2)) FF::template run<false, 1, F...>(v, lds, tid);
             FF::template store<RFL>(v, lds, tid);
@@ -1226,13 +1260,13 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
 #pragma unroll
             for (int ib = 0; ib < E / RF0; ++ib) {
                 const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
-                const uint32_t off = (uint32_t)((b ? rowB : rowA) * N2 + jj) * 8u;
+                const uint32_t off = spill_off(RP, j, b ? rowB : rowA, b, jj);
 #pragma unroll
-                for (int q = 0; q < RF0; ++q) Y.st2(v[ib * RF0 + q], off, q * LR * 8);
+                for (int q = 0; q < RF0; ++q) Y.st2(v[ib * RF0 + q], off, q * kQS);
             }
         }
         if (mask) {
-            const Buf V(k.Ym + (int64_t)pr * k.N, pbytes);
+            const Buf V(k.Ym + (int64_t)pr * pstride(k), pbytes);
             const Buf Ms(k.Mspec, pbytes);
 #pragma unroll
             for (int ib = 0; ib < E / RFL; ++ib) {
@@ -1262,9 +1296,9 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
 #pragma unroll
             for (int ib = 0; ib < E / RF0; ++ib) {
                 const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
-                const uint32_t off = (uint32_t)((b ? rowB : rowA) * N2 + jj) * 8u;
+                const uint32_t off = spill_off(RP, j, b ? rowB : rowA, b, jj);
 #pragma unroll
-                for (int q = 0; q < RF0; ++q) V.st2(v[ib * RF0 + q], off, q * LR * 8);
+                for (int q = 0; q < RF0; ++q) V.st2(v[ib * RF0 + q], off, q * kQS);
             }
         }
     }
@@ -1462,13 +1496,30 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             FF::template store<RFL>(v, lds, tid);
         }
         __syncthreads();
-        cf *Y = k.Yd + (int64_t)pr * k.N;
+        cf *Y = k.Yd + (int64_t)pr * pstride(k);
+        const int64_t RP = rpitch(k);
+        if constexpr (kPairIL) {
+            // item = (row pair p, 4 columns): 4 x 16 B = (row k1, row N1 - k1)
+            // of 4 consecutive columns, contiguous
+            for (int it = tid; it < N1 / 2 * (B / 4); it += T) {
+                const int pp = it / (B / 4);
+                const int b4 = (it - pp * (B / 4)) * 4;
+                const int ka = il_row(pp, 0, N1), kb = il_row(pp, 1, N1);
+                float4 *dst = reinterpret_cast<float4 *>(Y + ((int64_t)pp * RP + n20 + b4) * 2);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const cf a = lds[LdsC::at(b4 + i, ka)], b = lds[LdsC::at(b4 + i, kb)];
+                    dst[i] = make_float4(a.x, a.y, b.x, b.y);
+                }
+            }
+            return;
+        }
         for (int it = tid; it < N1 * B / 4; it += T) {
             const int k1 = it / (B / 4);
             const int b4 = (it - k1 * (B / 4)) * 4;
             cf a0 = lds[LdsC::at(b4 + 0, k1)], a1 = lds[LdsC::at(b4 + 1, k1)];
             cf a2 = lds[LdsC::at(b4 + 2, k1)], a3 = lds[LdsC::at(b4 + 3, k1)];
-            float4 *dst = reinterpret_cast<float4 *>(Y + (int64_t)k1 * N2 + n20 + b4);
+            float4 *dst = reinterpret_cast<float4 *>(Y + (int64_t)k1 * RP + n20 + b4);
             dst[0] = make_float4(a0.x, a0.y, a1.x, a1.y);
             dst[1] = make_float4(a2.x, a2.y, a3.x, a3.y);
         }
@@ -1483,13 +1534,42 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     __device__ static __forceinline__ void inv_block(const KP &k, const cf *Yp, int64_t n20, cf *lds, int tid) {
         const int64_t N2 = k.N2;
         const float invN = k.invN;
-        const Buf Y(Yp, (uint32_t)(N1 * N2 * 8));      // one pair spill, < 2^28 bytes
+        const Buf Y(Yp, (uint32_t)(pstride(k) * 8));   // one pair spill, < 2^28 bytes
+        const uint32_t RP = (uint32_t)rpitch(k);
         const uint32_t s0 = (uint32_t)n20 * 8u;        // wave-uniform part of the offset
+        if constexpr (kPairIL) {
+#pragma unroll 1
+            for (int it = tid; it < N1 / 2 * (B / 4); it += T) {
+                const int pp = it / (B / 4);
+                const int b4 = (it - pp * (B / 4)) * 4;
+                const uint32_t off = ((uint32_t)pp * RP + (uint32_t)b4) * 16u;
+                float4 q[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) q[i] = Y.ld4<PSS_SPILL_AUX>(off + 16u * i, 2u * s0);
+#pragma unroll
+                for (int side = 0; side < 2; ++side) {
+                    const int k1 = il_row(pp, side, N1);
+                    const uint32_t m0 = (uint32_t)(n20 + b4) * (uint32_t)k1;
+                    float r0 = (float)m0 * invN;
+                    if (r0 >= 0.5f) r0 -= 1.0f;
+                    float r1 = (float)k1 * invN;
+                    if (r1 >= 0.5f) r1 -= 1.0f;
+                    const cf w0 = expi_rev(r0), w1 = expi_rev(r1);
+                    const cf w2 = cmul(w1, w1);
+                    const cf tw[4] = {w0, cmul(w0, w1), cmul(w0, w2), cmul(w0, cmul(w2, w1))};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const cf a = side ? make_float2(q[i].z, q[i].w) : make_float2(q[i].x, q[i].y);
+                        if constexpr (!(kAbl & 4)) lds[LdsC::at(b4 + i, k1)] = cmul(a, tw[i]); else lds[LdsC::at(b4 + i, k1)] = a;
+                    }
+                }
+            }
+        } else {
 #pragma unroll 1
         for (int it = tid; it < N1 * B / 4; it += T) {
             const int k1 = it / (B / 4);
             const int b4 = (it - k1 * (B / 4)) * 4;
-            uint32_t off = ((uint32_t)k1 * (uint32_t)N2 + (uint32_t)b4) * 8u;
+            uint32_t off = ((uint32_t)k1 * RP + (uint32_t)b4) * 8u;
             uint32_t so = s0;
             if constexpr (kAbl & 128) {   // ablation: contiguous loads (wrong data)
                 off = (uint32_t)it * 32u;
@@ -1512,6 +1592,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             for (int i = 0; i < 4; ++i) {
                 if constexpr (!(kAbl & 4)) lds[LdsC::at(b4 + i, k1)] = cmul(a[i], tw[i]); else lds[LdsC::at(b4 + i, k1)] = a[i];
             }
+        }
         }
         __syncthreads();
         cf v[E];
@@ -1543,7 +1624,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         const int64_t n20 = (int64_t)cbx * B;
         const bool mask = k.mtab != 0;
         const float invN = k.invN;
-        inv_block(k, k.Yd + (int64_t)pr * k.N, n20, lds, tid);
+        inv_block(k, k.Yd + (int64_t)pr * pstride(k), n20, lds, tid);
 #pragma unroll 1
         for (int it = tid; it < N1 * B / 4; it += T) {
             const int n1 = it / (B / 4);
@@ -1584,7 +1665,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         const PssPipeline &p = k.p;
         const float invN = k.invN, nn = p.noise_norm;
         const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
-        inv_block(k, k.Yd + (int64_t)pr * k.N, n20, lds, tid);
+        inv_block(k, k.Yd + (int64_t)pr * pstride(k), n20, lds, tid);
         const Rng gn(p.seed, p.call_noise, P_NOISE);
         const uint32_t rbytes = (uint32_t)(k.N * 4);
         const Buf oa(p.data + (int64_t)max(ra, 0) * p.ld, rbytes), ob(p.data + (int64_t)min(rb, p.nchan - 1) * p.ld, rbytes);
@@ -1638,7 +1719,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         xcd_block(cbx, pr);
         const int64_t n20 = (int64_t)cbx * B;
         const float invN = k.invN;
-        inv_block(k, k.Ym + (int64_t)pr * k.N, n20, lds, tid);
+        inv_block(k, k.Ym + (int64_t)pr * pstride(k), n20, lds, tid);
         float *ra = nodes + (int64_t)(2 * pr) * k.N, *rb = ra + k.N;
         for (int it = tid; it < N1 * B / 4; it += T) {
             const int n1 = it / (B / 4);
@@ -2285,9 +2366,11 @@ static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
     int64_t o = 0;
     if (fourstep_len(N) && !filt) {
         const int64_t npairs = ((int64_t)nchan + 2) / 2;   // pairs of (even, odd) global channels
-        w.yd = o;    o += al256(npairs * N * 8);
+        // pair spills: N1 <= N / 1024 rows of N2 + kSpillPad on every 2^m split
+        const int64_t ps = N + (N / 1024) * kSpillPad;
+        w.yd = o;    o += al256(npairs * ps * 8);
         w.mspec = o; o += al256(N * 8);
-        w.ynode = o; o += al256((int64_t)(KCH / 2) * N * 8);
+        w.ynode = o; o += al256((int64_t)(KCH / 2) * ps * 8);
         w.nodes = o; o += al256((int64_t)KCH * N * 4);
         w.bits = o;  o += al256((N / 32) * 8);
         w.base = o;  o += al256((N / 32) * 4);
@@ -2499,7 +2582,7 @@ static int launch_batches(KP &k, hipStream_t st, int nb) {
         kb.p.nyq_im = k.p.nyq_im + r0;
         if (k.p.mask_ramp) kb.p.mask_ramp = k.p.mask_ramp + r0;
         kb.rtab = k.rtab + (int64_t)r0 * PR::RFL;
-        kb.Yd = k.Yd + (int64_t)p0 * k.N;
+        kb.Yd = k.Yd + (int64_t)p0 * pstride(k);
         kb.after_a = ss->ev[1 + b];
         hipStream_t sb = ss->s[b & 1];
         if (b > 0) HIPCHK(hipStreamWaitEvent(sb, ss->ev[b], 0));     // batch b-1's pass A done
@@ -2528,6 +2611,7 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
     char *w = reinterpret_cast<char *>(k.p.work);
     const WsLayout L = ws_layout(k.p.nchan, k.N);
     k.Yd = reinterpret_cast<cf *>(w + L.yd);
+    k.sp = ((N1 & (N1 - 1)) == 0) ? N2 + kSpillPad : N2;   // (ws_layout sizes the pad for 2^m)
     if (k.p.null_mode == PSS_NULL_DELAYED) {
         // the mask table's position arithmetic is for N = 2^m (validate()
         // sends delayed nulls of other lengths to the direct path)
