@@ -2525,9 +2525,16 @@ constexpr int xrs_write(int B) { return -1; }
 // channel): results are bitwise those of one launch.  Fork from / join to
 // the caller's stream with events, so the run stays stream-ordered.
 static int g_batches = -1;
+// PSS_BATCH_AFTER=row: batch b's pass A waits for batch b-1's ROW pass
+// instead, so it runs next to batch b-1's pass C (the VALU-bound generator
+// beside the memory-pattern-bound inverse columns; needs a pass C that leaves
+// LDS for a pass-A workgroup on the same CU, e.g. PSS_BC=8)
+static bool g_batch_after_row = false;
 static int batches_setting() {
     if (g_batches < 0) {
         const char *e = getenv("PSS_BATCHES");
+        const char *a = getenv("PSS_BATCH_AFTER");
+        g_batch_after_row = a && strcmp(a, "row") == 0;
         g_batches = e ? atoi(e) : 1;
         if (g_batches < 1) g_batches = 1;
         if (g_batches > 16) g_batches = 16;
@@ -2679,7 +2686,7 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     }
     tk_end(st);
     LAUNCHCHK();
-    if (k.after_a) HIPCHK(hipEventRecord(k.after_a, st));   // batching: the next batch's pass A may start
+    if (k.after_a && !g_batch_after_row) HIPCHK(hipEventRecord(k.after_a, st));   // batching: the next batch's pass A may start
     tk_begin(TK_ROW, st);
     if (k.p.tail_a)
         k_pair_row<PR, TR, true><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
@@ -2687,6 +2694,7 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
         k_pair_row<PR, TR><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
     tk_end(st);
     LAUNCHCHK();
+    if (k.after_a && g_batch_after_row) HIPCHK(hipEventRecord(k.after_a, st));
     const bool fast = PCC::kItemsExact && fast_epilogue(k);
     if (k.mask_ready && !fast) HIPCHK(hipStreamWaitEvent(st, k.mask_ready, 0));   // generic pass C reads the bits
     tk_begin(TK_COLC, st);
