@@ -64,6 +64,7 @@ struct Buf {
         u4 w = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX);
         return make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
     }
+    template <int AUX = 0>
     __device__ __forceinline__ void st4(float a, float b, float c, float d, uint32_t voff, uint32_t soff) const {
         typedef unsigned int u4 __attribute__((ext_vector_type(4)));
         u4 w;
@@ -71,7 +72,7 @@ struct Buf {
         w.y = __float_as_uint(b);
         w.z = __float_as_uint(c);
         w.w = __float_as_uint(d);
-        __builtin_amdgcn_raw_buffer_store_b128(w, r, voff, soff, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(w, r, voff, soff, AUX);
     }
 };
 

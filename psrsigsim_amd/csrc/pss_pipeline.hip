@@ -88,6 +88,15 @@ __device__ __forceinline__ int il_row(int p, int side, int N1) {
 #define PSS_SPILL_PAD 0
 #endif
 static constexpr int kSpillPad = PSS_SPILL_PAD;
+// cache policy bits of the fast pass C's output stores (experiment switch;
+// gfx950 buffer aux: 1 = sc0, 2 = nt, 16 = sc1)
+#ifndef PSS_OUT_AUX
+#define PSS_OUT_AUX 0
+#endif
+// pass A's spill stores non-temporal (experiment switch)
+#ifndef PSS_SPILL_NT
+#define PSS_SPILL_NT 0
+#endif
 // fast pass C block width / threads for N = 2^22 on the 512 x 8192 split
 #ifndef PSS_BC8
 #define PSS_BC8 16
@@ -1520,8 +1529,15 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             cf a0 = lds[LdsC::at(b4 + 0, k1)], a1 = lds[LdsC::at(b4 + 1, k1)];
             cf a2 = lds[LdsC::at(b4 + 2, k1)], a3 = lds[LdsC::at(b4 + 3, k1)];
             float4 *dst = reinterpret_cast<float4 *>(Y + (int64_t)k1 * RP + n20 + b4);
-            dst[0] = make_float4(a0.x, a0.y, a1.x, a1.y);
-            dst[1] = make_float4(a2.x, a2.y, a3.x, a3.y);
+            if constexpr (PSS_SPILL_NT) {
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                v4f *d4 = reinterpret_cast<v4f *>(dst);
+                __builtin_nontemporal_store((v4f){a0.x, a0.y, a1.x, a1.y}, d4);
+                __builtin_nontemporal_store((v4f){a2.x, a2.y, a3.x, a3.y}, d4 + 1);
+            } else {
+                dst[0] = make_float4(a0.x, a0.y, a1.x, a1.y);
+                dst[1] = make_float4(a2.x, a2.y, a3.x, a3.y);
+            }
         }
     }
 
@@ -1705,8 +1721,8 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                 if (hasb) ob.st4(acc[t][1][0], acc[t][1][1], acc[t][1][2], acc[t][1][3], o2, 0);
                 continue;
             }
-            if (hasa) oa.st4(acc[t][0][0], acc[t][0][1], acc[t][0][2], acc[t][0][3], off, 0);
-            if (hasb) ob.st4(acc[t][1][0], acc[t][1][1], acc[t][1][2], acc[t][1][3], off, 0);
+            if (hasa) oa.st4<PSS_OUT_AUX>(acc[t][0][0], acc[t][0][1], acc[t][0][2], acc[t][0][3], off, 0);
+            if (hasb) ob.st4<PSS_OUT_AUX>(acc[t][1][0], acc[t][1][1], acc[t][1][2], acc[t][1][3], off, 0);
         }
     }
 
