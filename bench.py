@@ -417,15 +417,26 @@ def main():
         _lib.load().pss_timing_enable(1)
         _lib.timing_collect()
     t0 = time.perf_counter()
+    # stream-ordered step boundaries (the engine launches on the current
+    # stream): the first step's span includes its host planning on an idle
+    # GPU, the later ones are the steady state
+    evs = []
+    if not args.dry_run:
+        evs.append(torch.cuda.Event(enable_timing=True))
+        evs[-1].record()
     marks = []
     for _ in range(args.steps):
         s = step()
         if args.workload == "c4":
             _ = s.data          # fold-mode output is small: materialise it (the gather did when N > 1)
         del s
+        if evs:
+            evs.append(torch.cuda.Event(enable_timing=True))
+            evs[-1].record()
         marks.append(time.perf_counter())
     sync()
     t1 = time.perf_counter()
+    spans = [a.elapsed_time(b) for a, b in zip(evs, evs[1:])]
     if args.verbose:
         prev = t0
         for i, m in enumerate(marks):
@@ -507,6 +518,8 @@ def main():
                        "nchan_per_gpu": C, "nsamp": nsamp, "parallelism": "channel-shard x%d" % world},
             "ranks": ranks,
             "gpu_kernel_ms_per_step": round(gpu_ms, 3),
+            "step_ms_first": round(spans[0], 3) if spans else None,
+            "step_ms_steady": round(float(np.median(spans[1:])), 3) if len(spans) > 1 else None,
             "kernels": kernels,
             "roofline": roof,
             "cpu_baseline": cpu,
