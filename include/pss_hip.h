@@ -236,7 +236,9 @@ int pss_down_sample(const float *in, float *out, int32_t nrows, int64_t in_len,
                     int64_t in_ld, int32_t fact, void *stream);
 
 /* utils.rebin per row (utils/utils.py:71-91): `lo`/`hi` are the integer window
- * edges [lo_i, hi_i) the reference derives from its ceil() arithmetic. */
+ * edges [lo_i, hi_i) the reference derives from its ceil() arithmetic, device
+ * arrays of `newlen` entries with 0 <= lo_i <= hi_i <= in_len (not checked:
+ * they live on the device).  PSS_EINVAL on NULL pointers or in_ld < in_len. */
 int pss_rebin(const float *in, float *out, int32_t nrows, int64_t in_len, int64_t in_ld,
               int32_t newlen, const int64_t *lo, const int64_t *hi, void *stream);
 

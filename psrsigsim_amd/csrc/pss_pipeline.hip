@@ -3205,6 +3205,9 @@ int pss_down_sample(const float *in, float *out, int32_t nrows, int64_t in_len, 
                     int32_t fact, void *stream) {
     if (fact < 1 || in_len % fact) return fail(PSS_EINVAL, "down_sample: %lld %% %d != 0", (long long)in_len, fact);
     if (nrows <= 0) return PSS_OK;
+    if (!in || !out) return fail(PSS_EINVAL, "down_sample: NULL argument");
+    if (in_ld < in_len) return fail(PSS_EINVAL, "down_sample: in_ld < in_len");
+    if (nrows > 65535) return fail(PSS_EINVAL, "nchan %d > 65535 per launch", nrows);
     dim3 g = stream_grid(in_len / fact, nrows);
     hipLaunchKernelGGL(k_down_sample, g, dim3(256), 0, (hipStream_t)stream, in, out, in_len, in_ld, fact);
     LAUNCHCHK();
@@ -3213,8 +3216,11 @@ int pss_down_sample(const float *in, float *out, int32_t nrows, int64_t in_len, 
 
 int pss_rebin(const float *in, float *out, int32_t nrows, int64_t in_len, int64_t in_ld, int32_t newlen,
               const int64_t *lo, const int64_t *hi, void *stream) {
-    (void)in_len;
     if (nrows <= 0 || newlen <= 0) return PSS_OK;
+    // lo / hi are device arrays (the caller's windows, 0 <= lo_i <= hi_i <= in_len)
+    if (!in || !out || !lo || !hi) return fail(PSS_EINVAL, "rebin: NULL argument");
+    if (in_ld < in_len) return fail(PSS_EINVAL, "rebin: in_ld < in_len");
+    if (nrows > 65535) return fail(PSS_EINVAL, "nchan %d > 65535 per launch", nrows);
     dim3 g = stream_grid(newlen, nrows);
     hipLaunchKernelGGL(k_rebin, g, dim3(256), 0, (hipStream_t)stream, in, out, in_ld, newlen, lo, hi);
     LAUNCHCHK();
@@ -3224,6 +3230,7 @@ int pss_rebin(const float *in, float *out, int32_t nrows, int64_t in_len, int64_
 int pss_clip_cast(const float *in, void *out, int64_t count, float clip, int32_t out_kind, void *stream) {
     if (out_kind != PSS_OUT_F32 && out_kind != PSS_OUT_I8) return fail(PSS_EINVAL, "out_kind");
     if (count <= 0) return PSS_OK;
+    if (!in || !out) return fail(PSS_EINVAL, "clip_cast: NULL argument");
     dim3 g = stream_grid(count, 1);
     hipLaunchKernelGGL(k_clip_cast, g, dim3(256), 0, (hipStream_t)stream, in, out, count, clip, out_kind);
     LAUNCHCHK();
@@ -3236,6 +3243,7 @@ int pss_fold(const float *data, float *out, int32_t nchan, int64_t ld, int64_t n
     if (npbins + n_fold * (npbins / 2) > ld)
         return fail(PSS_EINVAL, "fold: %lld + %lld x %lld samples exceed the row (ld %lld)", (long long)npbins,
                     (long long)n_fold, (long long)(npbins / 2), (long long)ld);
+    if (!data || !out || nchan > 65535) return fail(PSS_EINVAL, "fold: NULL argument or nchan > 65535");
     dim3 g = stream_grid(npbins / 2, nchan);
     hipLaunchKernelGGL(k_fold, g, dim3(256), 0, (hipStream_t)stream, data, out, ld, npbins, n_fold);
     LAUNCHCHK();
@@ -3245,6 +3253,7 @@ int pss_fold(const float *data, float *out, int32_t nchan, int64_t ld, int64_t n
 int pss_fold_periods(const float *data, float *out, int32_t nchan, int64_t ld, int64_t nbin, int64_t nper,
                      void *stream) {
     if (nchan <= 0 || nbin < 1 || nper < 1) return fail(PSS_EINVAL, "fold geometry");
+    if (!data || !out || nchan > 65535) return fail(PSS_EINVAL, "fold: NULL argument or nchan > 65535");
     if (nper * nbin > ld) return fail(PSS_EINVAL, "fold: %lld periods of %lld bins exceed the row", (long long)nper,
                                       (long long)nbin);
     dim3 g = stream_grid(nbin, nchan);
@@ -3263,6 +3272,7 @@ int pss_null_shift(const float *row, int64_t count, int64_t *out, void *stream) 
 int pss_chi2_fill(float *out, int32_t nrows, int32_t chan0, int64_t n, float df, uint64_t seed,
                   uint32_t call_id, uint32_t purpose, void *stream) {
     if (nrows <= 0 || n <= 0) return PSS_OK;
+    if (!out || nrows > 65535) return fail(PSS_EINVAL, "chi2_fill: NULL out or nrows > 65535");
     dim3 g = stream_grid((n + 3) / 4, nrows);
     hipLaunchKernelGGL(k_chi2_fill, g, dim3(256), 0, (hipStream_t)stream, out, n, chan0, df, seed,
                        call_id, purpose);

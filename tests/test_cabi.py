@@ -110,3 +110,21 @@ def test_fold_rejects_out_of_row_geometry():
     assert L.pss_fold(None, None, 0, 100, 64, 1, None) == _lib.PSS_EINVAL     # no rows
     L.pss_fold(None, None, 2, 100, 64, 3, None)
     assert "exceed the row" in _lib.last_error()
+
+
+def test_aux_entry_points_validate_arguments():
+    """The resampling / cast / draw entry points reject NULL buffers and rows
+    shorter than the data before any launch (no GPU touched)."""
+    import ctypes
+    L = _lib.load()
+    host = (ctypes.c_float * 16)()
+    p = ctypes.cast(host, ctypes.c_void_p)
+    assert L.pss_down_sample(None, None, 2, 100, 100, 2, None) == _lib.PSS_EINVAL
+    assert L.pss_down_sample(p, p, 2, 100, 50, 2, None) == _lib.PSS_EINVAL          # in_ld < in_len
+    assert "in_ld < in_len" in _lib.last_error()
+    assert L.pss_down_sample(p, p, 2, 100, 100, 3, None) == _lib.PSS_EINVAL         # 3 does not divide 100
+    assert L.pss_rebin(None, None, 2, 100, 100, 10, None, None, None) == _lib.PSS_EINVAL
+    assert L.pss_rebin(p, p, 2, 100, 50, 10, p, p, None) == _lib.PSS_EINVAL         # in_ld < in_len
+    assert L.pss_clip_cast(None, None, 10, 200.0, _lib.OUT_F32, None) == _lib.PSS_EINVAL
+    assert L.pss_chi2_fill(None, 2, 0, 16, 1.0, 1, 0, 0, None) == _lib.PSS_EINVAL
+    assert L.pss_fold_periods(None, None, 2, 100, 10, 5, None) == _lib.PSS_EINVAL
