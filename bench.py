@@ -279,6 +279,66 @@ def _free_port():
     return port
 
 
+class PowerSampler:
+    """Socket power and gfx clock of this rank's GPU (amdsmi), sampled by a
+    daemon thread every `period` s through the timed region: the C3 step runs
+    at the power limit with sclk held near 2.1 GHz.  Any
+    failure (no amdsmi, no matching device) leaves the bench line's field null."""
+
+    def __init__(self, dev, period=0.05):
+        import threading
+        self.samples = []
+        self.limit_w = None
+        self._stop = threading.Event()
+        self._thread = None
+        try:
+            import amdsmi
+            import torch
+            amdsmi.amdsmi_init()
+            bus = torch.cuda.get_device_properties(dev).pci_bus_id
+            self._smi = amdsmi
+            self._h = None
+            for h in amdsmi.amdsmi_get_processor_handles():
+                if int(amdsmi.amdsmi_get_gpu_device_bdf(h).split(":")[1], 16) == bus:
+                    self._h = h
+            if self._h is None:
+                return
+            lim = amdsmi.amdsmi_get_power_info(self._h).get("power_limit")
+            self.limit_w = lim / 1e6 if isinstance(lim, (int, float)) else None
+            self._thread = threading.Thread(target=self._run, args=(period,), daemon=True)
+        except Exception:
+            self._thread = None
+
+    def _run(self, period):
+        while not self._stop.is_set():
+            try:
+                w = self._smi.amdsmi_get_power_info(self._h).get("current_socket_power")
+                c = self._smi.amdsmi_get_clock_info(self._h, self._smi.AmdSmiClkType.GFX).get("clk")
+                if isinstance(w, (int, float)) and isinstance(c, (int, float)):
+                    self.samples.append((float(w), float(c)))
+            except Exception:
+                return
+            self._stop.wait(period)
+
+    def start(self):
+        if self._thread is not None:
+            self._thread.start()
+
+    def stop(self):
+        if self._thread is not None:
+            self._stop.set()
+            self._thread.join(timeout=2.0)
+
+    def report(self):
+        if len(self.samples) < 3:
+            return None
+        w = np.array([a for a, _ in self.samples])
+        c = np.array([b for _, b in self.samples])
+        return {"socket_w_median": round(float(np.median(w)), 1), "socket_w_max": round(float(w.max()), 1),
+                "power_limit_w": self.limit_w, "sclk_mhz_median": round(float(np.median(c)), 1),
+                "samples": len(self.samples), "source": "amdsmi, every 50 ms through the timed steps"}
+
+
 def launch_ranks(n):
     """Start one rank per GPU (torch.distributed.run, 127.0.0.1) as a child
     process running this same command line, and return its exit status.
@@ -416,6 +476,9 @@ def main():
     if not args.dry_run:
         _lib.load().pss_timing_enable(1)
         _lib.timing_collect()
+    power = None if args.dry_run else PowerSampler(torch.cuda.current_device())
+    if power is not None:
+        power.start()
     t0 = time.perf_counter()
     # stream-ordered step boundaries (the engine launches on the current
     # stream): the first step's span includes its host planning on an idle
@@ -436,6 +499,8 @@ def main():
         marks.append(time.perf_counter())
     sync()
     t1 = time.perf_counter()
+    if power is not None:
+        power.stop()
     spans = [a.elapsed_time(b) for a, b in zip(evs, evs[1:])]
     if args.verbose:
         prev = t0
@@ -520,6 +585,7 @@ def main():
             "gpu_kernel_ms_per_step": round(gpu_ms, 3),
             "step_ms_first": round(spans[0], 3) if spans else None,
             "step_ms_steady": round(float(np.median(spans[1:])), 3) if len(spans) > 1 else None,
+            "gpu_power": power.report() if power is not None else None,
             "kernels": kernels,
             "roofline": roof,
             "cpu_baseline": cpu,
