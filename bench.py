@@ -299,8 +299,11 @@ class PowerSampler:
             self._smi = amdsmi
             self._h = None
             for h in amdsmi.amdsmi_get_processor_handles():
-                if int(amdsmi.amdsmi_get_gpu_device_bdf(h).split(":")[1], 16) == bus:
-                    self._h = h
+                try:
+                    if int(amdsmi.amdsmi_get_gpu_device_bdf(h).split(":")[1], 16) == bus:
+                        self._h = h
+                except Exception:
+                    continue
             if self._h is None:
                 return
             lim = amdsmi.amdsmi_get_power_info(self._h).get("power_limit")
