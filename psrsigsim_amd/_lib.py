@@ -107,10 +107,11 @@ def check_build_hash(path=LIB_PATH):
     from . import build as _b
     try:
         want = _b.source_hash()
+        want_debug = _b.source_hash(["-DPSS_DEBUG=1"])   # the device-assert build (build --debug)
     except OSError:
         return          # sources not shipped: nothing to compare against
     got = _b.embedded_hash(path)
-    if got != want:
+    if got not in (want, want_debug):
         raise HipUnavailable("%s was built from other sources (hash %s, tree %s) -- rebuild with "
                              "psrsigsim_amd/build.py" % (path, got, want))
 

@@ -18,6 +18,7 @@ SRC = [os.path.join(HERE, "csrc", "pss_pipeline.hip"), os.path.join(HERE, "csrc"
 DEPS = SRC + [os.path.join(HERE, "csrc", f) for f in ("pss_device.hpp", "pss_fft.hpp")] + \
     [os.path.join(ROOT, "include", "pss_hip.h")]
 OUT = os.path.join(HERE, "libpss_hip.so")
+OUT_DEBUG = os.path.join(HERE, "libpss_hip_debug.so")
 ARCH = os.environ.get("PSS_OFFLOAD_ARCH", "gfx950")
 # -fno-slp-vectorize: packed f32 (v_pk_*) issues at half rate on gfx950 and
 # costs register-pair moves; scalar f32 is cheaper here.
@@ -49,18 +50,23 @@ def stale():
     return embedded_hash() != source_hash()
 
 
-def build(force=False, verbose=True):
-    if not force and not stale():
-        return OUT
+def build(force=False, verbose=True, debug=False):
+    """Build the product library, or with ``debug=True`` the device-assert
+    build ``libpss_hip_debug.so`` (PSS_DEBUG=1: bounds asserts on generic and
+    buffer accesses; load it with PSS_LIB_PATH, tools/debug_gpu.sh)."""
+    extra = ["-DPSS_DEBUG=1"] if debug else []
+    out = OUT_DEBUG if debug else OUT
+    if not force and embedded_hash(out) == source_hash(extra):
+        return out
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc] + FLAGS + ['-DPSS_BUILD_HASH="%s"' % source_hash(),
-                             "-I" + os.path.join(ROOT, "include"), "-o", OUT + ".tmp"] + SRC
+    cmd = [hipcc] + FLAGS + extra + ['-DPSS_BUILD_HASH="%s"' % source_hash(extra),
+                                     "-I" + os.path.join(ROOT, "include"), "-o", out + ".tmp"] + SRC
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, debug="--debug" in sys.argv)

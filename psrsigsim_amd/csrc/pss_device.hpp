@@ -4,6 +4,20 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Debug builds (PSS_DEBUG=1, tools/debug_gpu.sh): device-side bounds asserts
+// on the generic-pointer accesses and on the offsets of buffer (SRD) accesses
+// -- the hardware drops an out-of-range buffer store and returns 0 for an
+// out-of-range load silently, so a wrong offset would otherwise go unseen.
+#ifndef PSS_DEBUG
+#define PSS_DEBUG 0
+#endif
+#if PSS_DEBUG
+#include <cassert>
+#define PSS_DASSERT(c) assert(c)
+#else
+#define PSS_DASSERT(c) ((void)0)
+#endif
+
 namespace pss {
 
 typedef float2 cf;
@@ -43,15 +57,25 @@ __device__ __forceinline__ float fix_to_rev(uint64_t ph) {
 // --------------------------------------------------------------------------
 struct Buf {
     __amdgpu_buffer_rsrc_t r;
+#if PSS_DEBUG
+    uint32_t nbytes;
+    __device__ __forceinline__ Buf(const void *base, uint32_t bytes)
+        : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, bytes, 0x00020000)), nbytes(bytes) {}
+#define PSS_BUF_CHECK(voff, soff, w) PSS_DASSERT((uint64_t)(voff) + (soff) + (w) <= nbytes)
+#else
     __device__ __forceinline__ Buf(const void *base, uint32_t bytes)
         : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, bytes, 0x00020000)) {}
+#define PSS_BUF_CHECK(voff, soff, w) ((void)0)
+#endif
     __device__ __forceinline__ cf ld2(uint32_t voff, uint32_t soff) const {
         typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+        PSS_BUF_CHECK(voff, soff, 8);
         u2 w = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
         return make_float2(__uint_as_float(w.x), __uint_as_float(w.y));
     }
     __device__ __forceinline__ void st2(cf v, uint32_t voff, uint32_t soff) const {
         typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+        PSS_BUF_CHECK(voff, soff, 8);
         u2 w;
         w.x = __float_as_uint(v.x);
         w.y = __float_as_uint(v.y);
@@ -61,6 +85,7 @@ struct Buf {
     template <int AUX = 0>
     __device__ __forceinline__ float4 ld4(uint32_t voff, uint32_t soff) const {
         typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+        PSS_BUF_CHECK(voff, soff, 16);
         u4 w = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX);
         return make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
     }
@@ -72,6 +97,7 @@ struct Buf {
         w.y = __float_as_uint(b);
         w.z = __float_as_uint(c);
         w.w = __float_as_uint(d);
+        PSS_BUF_CHECK(voff, soff, 16);
         __builtin_amdgcn_raw_buffer_store_b128(w, r, voff, soff, AUX);
     }
 };

@@ -476,6 +476,7 @@ __global__ __launch_bounds__(256) void k_null_fix_list(KP k) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         for (uint32_t e = (uint32_t)lane; e < total; e += 64u) {
             const uint32_t h = desc[wv][e], nb = dbase[wv][e];
+            PSS_DASSERT((int64_t)nb + 4 <= k.N && (nb & 3u) == 0u);
             const float4 xn = chi2_1x4(gn.bits(nb >> 2, c, 0u));
             const float4 xr = chi2_1x4(gr.bits(nb >> 2, c, 0u));
             const float vn[4] = {xn.x, xn.y, xn.z, xn.w}, vr[4] = {xr.x, xr.y, xr.z, xr.w};
@@ -672,6 +673,7 @@ __device__ __forceinline__ void source4(const KP &k, int r, int64_t n0, int cnt,
                                         bool want_im = true) {
     const PssPipeline &p = k.p;
     const uint32_t c = (uint32_t)(p.chan0 + r);
+    PSS_DASSERT(r >= 0 && r < p.nchan && n0 >= 0 && n0 + cnt <= k.N);
 #pragma unroll
     for (int i = 0; i < 4; ++i) { re[i] = 0.f; im[i] = 0.f; }
     if (want_re) {
@@ -745,6 +747,7 @@ __device__ __forceinline__ void epilogue4(const KP &k, int r, int64_t n0, int cn
     const PssPipeline &p = k.p;
     const uint32_t c = (uint32_t)(p.chan0 + r);
     float *row = p.data + (int64_t)r * p.ld;
+    PSS_DASSERT(r >= 0 && r < p.nchan && n0 >= 0 && n0 + cnt <= k.N);
     if (load_data) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) if (i < cnt) pre[i] = row[n0 + i];
@@ -1276,7 +1279,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
         }
         if (mask) {
             const Buf V(k.Ym + (int64_t)pr * pstride(k), pbytes);
-            const Buf Ms(k.Mspec, pbytes);
+            const Buf Ms(k.Mspec, (uint32_t)(k.N * 8));      // [N1][N2], no spill pad
 #pragma unroll
             for (int ib = 0; ib < E / RFL; ++ib) {
                 const int jg = tid + ib * T, b = jg / LRL, jj = jg - b * LRL;
@@ -1514,6 +1517,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                 const int pp = it / (B / 4);
                 const int b4 = (it - pp * (B / 4)) * 4;
                 const int ka = il_row(pp, 0, N1), kb = il_row(pp, 1, N1);
+                PSS_DASSERT(((int64_t)pp * RP + n20 + b4 + 4) * 2 <= pstride(k));
                 float4 *dst = reinterpret_cast<float4 *>(Y + ((int64_t)pp * RP + n20 + b4) * 2);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
@@ -1528,6 +1532,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             const int b4 = (it - k1 * (B / 4)) * 4;
             cf a0 = lds[LdsC::at(b4 + 0, k1)], a1 = lds[LdsC::at(b4 + 1, k1)];
             cf a2 = lds[LdsC::at(b4 + 2, k1)], a3 = lds[LdsC::at(b4 + 3, k1)];
+            PSS_DASSERT((int64_t)k1 * RP + n20 + b4 + 4 <= pstride(k));
             float4 *dst = reinterpret_cast<float4 *>(Y + (int64_t)k1 * RP + n20 + b4);
             if constexpr (PSS_SPILL_NT) {
                 typedef float v4f __attribute__((ext_vector_type(4)));
@@ -2174,6 +2179,7 @@ __global__ void k_rebin(const float *in, float *out, int64_t in_ld, int32_t newl
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < newlen; i += gridDim.x * blockDim.x) {
         double s = 0.0;
         const int64_t a = lo[i], b = hi[i];
+        PSS_DASSERT(a >= 0 && a <= b && b <= in_ld);
         for (int64_t j = a; j < b; ++j) s += row[j];
         out[(int64_t)r * newlen + i] = (b > a) ? (float)(s / (double)(b - a)) : NAN;
     }
