@@ -93,6 +93,17 @@ static constexpr int kSpillPad = PSS_SPILL_PAD;
 #ifndef PSS_OUT_AUX
 #define PSS_OUT_AUX 0
 #endif
+// Delayed null fused into the fast pass C (1): each item looks its 4 samples
+// up in the mask table and stores replacement + noise where nulled, so no
+// separate fix-up pass rewrites them; 0 (product): k_null_fix_list
+// afterwards.  Measured (C3, one box): fused pass C 27.0 ms against 16.6 +
+// 2.5 for pass C + fix-up -- the per-lane table lookups 8192 samples apart
+// and the f-dependent positions, divergent in every wave, cost far more than
+// the fix-up's compacted pass (bitwise the same results; 138 GPU tests).
+#ifndef PSS_FUSE_NULL
+#define PSS_FUSE_NULL 0
+#endif
+static constexpr bool kFuseNull = PSS_FUSE_NULL != 0;
 // pass A's spill stores non-temporal (experiment switch)
 #ifndef PSS_SPILL_NT
 #define PSS_SPILL_NT 0
@@ -1670,9 +1681,10 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
 
     // C, fast path (host-selected: Philox draws with df = 1 for noise and
     // null replacement, no injected draws, no observe() copy).  Bitwise equal
-    // to passC.  Every sample is stored as signal + noise; the nulled samples
-    // of a delayed null are rewritten afterwards by k_null_fix (~10% of the
-    // samples; scattered 8192 apart in this kernel's column order).
+    // to passC.  Every sample is stored as signal + noise, or, at the
+    // positions a delayed null's mask table marks for its channel (PSS_FUSE_NULL),
+    // as replacement + noise; with PSS_FUSE_NULL=0 those are rewritten
+    // afterwards by k_null_fix_list instead.
     __device__ static void passC_fast(const KP &k) {
         static_assert(kItemsExact, "fast pass C: whole items per thread");
         __shared__ __align__(16) cf lds[B * LdsC::RS];
@@ -1688,6 +1700,16 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
         inv_block(k, k.Yd + (int64_t)pr * pstride(k), n20, lds, tid);
         const Rng gn(p.seed, p.call_noise, P_NOISE);
+        // fused delayed null (kFuseNull): the channels' table splits
+        const bool mnull = kFuseNull && k.mtab;
+        uint32_t isa = 0, isb = 0;
+        float tma = 0.f, tmb = 0.f;
+        if (mnull) {
+            if (hasa) mask_split((uint64_t)p.mask_ramp[ra], k.log2n, isa, tma);
+            if (hasb) mask_split((uint64_t)p.mask_ramp[rb], k.log2n, isb, tmb);
+        }
+        const Rng gr(p.seed, p.call_null, P_REP);
+        const float sc = p.null_rep_scale;
         const uint32_t rbytes = (uint32_t)(k.N * 4);
         const Buf oa(p.data + (int64_t)max(ra, 0) * p.ld, rbytes), ob(p.data + (int64_t)min(rb, p.nchan - 1) * p.ld, rbytes);
         float acc[ITEMS][2][4];
@@ -1712,6 +1734,26 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                 const cf z = lds[LdsC::at(b4 + i, n1)];
                 acc[t][0][i] = fmaf(nn, na[i], z.x * invN);
                 acc[t][1][i] = fmaf(nn, nb[i], z.y * invN);
+            }
+            if (mnull) {
+                // nulled samples: replacement + noise, the draws and
+                // expression of epilogue4 / k_null_fix_list (bitwise equal)
+                const uint32_t ha = hasa ? mask_hits4(k, (int64_t)n, isa, tma) : 0u;
+                const uint32_t hb = hasb ? mask_hits4(k, (int64_t)n, isb, tmb) : 0u;
+                if (ha) {
+                    const float4 r = chi2_1x4(gr.bits(n >> 2, ca, 0u));
+                    const float vr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if ((ha >> i) & 1u) acc[t][0][i] = fmaf(nn, na[i], vr[i] * sc);
+                }
+                if (hb) {
+                    const float4 r = chi2_1x4(gr.bits(n >> 2, cb, 0u));
+                    const float vr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if ((hb >> i) & 1u) acc[t][1][i] = fmaf(nn, nb[i], vr[i] * sc);
+                }
             }
         }
 #pragma unroll
@@ -2718,7 +2760,8 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     LAUNCHCHK();
     if (k.after_a && g_batch_after_row) HIPCHK(hipEventRecord(k.after_a, st));
     const bool fast = PCC::kItemsExact && fast_epilogue(k);
-    if (k.mask_ready && !fast) HIPCHK(hipStreamWaitEvent(st, k.mask_ready, 0));   // generic pass C reads the bits
+    // the generic pass C reads the bits, the fused fast one the table
+    if (k.mask_ready && (!fast || kFuseNull)) HIPCHK(hipStreamWaitEvent(st, k.mask_ready, 0));
     tk_begin(TK_COLC, st);
     if (fast) {
         if constexpr (PCC::kItemsExact)
@@ -2728,7 +2771,7 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     }
     tk_end(st);
     LAUNCHCHK();
-    if (fast && k.mtab) {
+    if (fast && k.mtab && !kFuseNull) {
         if (k.mask_ready) HIPCHK(hipStreamWaitEvent(st, k.mask_ready, 0));
         tk_begin(TK_NULLFIX, st);
         if (PSS_NULL_LIST) {
