@@ -28,6 +28,10 @@ typedef float2 cf;
 __device__ __forceinline__ cf cmul(cf a, cf b) {
     return make_float2(fmaf(a.x, b.x, -(a.y * b.y)), fmaf(a.x, b.y, a.y * b.x));
 }
+// a * conj(b), the same fused form
+__device__ __forceinline__ cf cmul_conj(cf a, cf b) {
+    return make_float2(fmaf(a.x, b.x, a.y * b.y), fmaf(a.y, b.x, -(a.x * b.y)));
+}
 __device__ __forceinline__ cf cadd(cf a, cf b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ cf csub(cf a, cf b) { return make_float2(a.x - b.x, a.y - b.y); }
 

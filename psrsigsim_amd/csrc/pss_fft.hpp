@@ -167,6 +167,89 @@ __device__ __forceinline__ void stage_sync() {
     }
 }
 
+// Twiddle table of the radix-16-after-16 stage: tw16[k * kTw16Pitch + q] =
+// e^{-2 pi i k q / 256}, k, q < 16 (row pitch 17: rows start on different
+// banks).  Filled once per workgroup from kCos256 (correctly rounded fp32,
+// below the native sincos' 1.2e-7 error).
+#ifndef PSS_TW16
+#define PSS_TW16 1      // experiment switch: 0 = native-sincos twiddles in every stage
+#endif
+static constexpr int kTw16Pitch = 17;
+static constexpr int kTw16Size = 16 * kTw16Pitch;
+// cos(2 pi m / 256), m = 0..255, correctly rounded to fp32 (float64 cos;
+// exactly 0/+-1 at multiples of pi/2)
+__device__ constexpr float kCos256[256] = {
+    1.000000000e+00f, 9.996988177e-01f, 9.987954497e-01f, 9.972904325e-01f,
+    9.951847196e-01f, 9.924795628e-01f, 9.891765118e-01f, 9.852776527e-01f,
+    9.807852507e-01f, 9.757021070e-01f, 9.700312614e-01f, 9.637760520e-01f,
+    9.569403529e-01f, 9.495281577e-01f, 9.415440559e-01f, 9.329928160e-01f,
+    9.238795042e-01f, 9.142097831e-01f, 9.039893150e-01f, 8.932242990e-01f,
+    8.819212914e-01f, 8.700869679e-01f, 8.577286005e-01f, 8.448535800e-01f,
+    8.314695954e-01f, 8.175848126e-01f, 8.032075167e-01f, 7.883464098e-01f,
+    7.730104327e-01f, 7.572088242e-01f, 7.409511209e-01f, 7.242470980e-01f,
+    7.071067691e-01f, 6.895405650e-01f, 6.715589762e-01f, 6.531728506e-01f,
+    6.343932748e-01f, 6.152315736e-01f, 5.956993103e-01f, 5.758081675e-01f,
+    5.555702448e-01f, 5.349976420e-01f, 5.141027570e-01f, 4.928981960e-01f,
+    4.713967443e-01f, 4.496113360e-01f, 4.275550842e-01f, 4.052413106e-01f,
+    3.826834261e-01f, 3.598950505e-01f, 3.368898630e-01f, 3.136817515e-01f,
+    2.902846634e-01f, 2.667127550e-01f, 2.429801822e-01f, 2.191012353e-01f,
+    1.950903237e-01f, 1.709618866e-01f, 1.467304677e-01f, 1.224106774e-01f,
+    9.801714122e-02f, 7.356456667e-02f, 4.906767607e-02f, 2.454122901e-02f,
+    0.000000000e+00f, -2.454122901e-02f, -4.906767607e-02f, -7.356456667e-02f,
+    -9.801714122e-02f, -1.224106774e-01f, -1.467304677e-01f, -1.709618866e-01f,
+    -1.950903237e-01f, -2.191012353e-01f, -2.429801822e-01f, -2.667127550e-01f,
+    -2.902846634e-01f, -3.136817515e-01f, -3.368898630e-01f, -3.598950505e-01f,
+    -3.826834261e-01f, -4.052413106e-01f, -4.275550842e-01f, -4.496113360e-01f,
+    -4.713967443e-01f, -4.928981960e-01f, -5.141027570e-01f, -5.349976420e-01f,
+    -5.555702448e-01f, -5.758081675e-01f, -5.956993103e-01f, -6.152315736e-01f,
+    -6.343932748e-01f, -6.531728506e-01f, -6.715589762e-01f, -6.895405650e-01f,
+    -7.071067691e-01f, -7.242470980e-01f, -7.409511209e-01f, -7.572088242e-01f,
+    -7.730104327e-01f, -7.883464098e-01f, -8.032075167e-01f, -8.175848126e-01f,
+    -8.314695954e-01f, -8.448535800e-01f, -8.577286005e-01f, -8.700869679e-01f,
+    -8.819212914e-01f, -8.932242990e-01f, -9.039893150e-01f, -9.142097831e-01f,
+    -9.238795042e-01f, -9.329928160e-01f, -9.415440559e-01f, -9.495281577e-01f,
+    -9.569403529e-01f, -9.637760520e-01f, -9.700312614e-01f, -9.757021070e-01f,
+    -9.807852507e-01f, -9.852776527e-01f, -9.891765118e-01f, -9.924795628e-01f,
+    -9.951847196e-01f, -9.972904325e-01f, -9.987954497e-01f, -9.996988177e-01f,
+    -1.000000000e+00f, -9.996988177e-01f, -9.987954497e-01f, -9.972904325e-01f,
+    -9.951847196e-01f, -9.924795628e-01f, -9.891765118e-01f, -9.852776527e-01f,
+    -9.807852507e-01f, -9.757021070e-01f, -9.700312614e-01f, -9.637760520e-01f,
+    -9.569403529e-01f, -9.495281577e-01f, -9.415440559e-01f, -9.329928160e-01f,
+    -9.238795042e-01f, -9.142097831e-01f, -9.039893150e-01f, -8.932242990e-01f,
+    -8.819212914e-01f, -8.700869679e-01f, -8.577286005e-01f, -8.448535800e-01f,
+    -8.314695954e-01f, -8.175848126e-01f, -8.032075167e-01f, -7.883464098e-01f,
+    -7.730104327e-01f, -7.572088242e-01f, -7.409511209e-01f, -7.242470980e-01f,
+    -7.071067691e-01f, -6.895405650e-01f, -6.715589762e-01f, -6.531728506e-01f,
+    -6.343932748e-01f, -6.152315736e-01f, -5.956993103e-01f, -5.758081675e-01f,
+    -5.555702448e-01f, -5.349976420e-01f, -5.141027570e-01f, -4.928981960e-01f,
+    -4.713967443e-01f, -4.496113360e-01f, -4.275550842e-01f, -4.052413106e-01f,
+    -3.826834261e-01f, -3.598950505e-01f, -3.368898630e-01f, -3.136817515e-01f,
+    -2.902846634e-01f, -2.667127550e-01f, -2.429801822e-01f, -2.191012353e-01f,
+    -1.950903237e-01f, -1.709618866e-01f, -1.467304677e-01f, -1.224106774e-01f,
+    -9.801714122e-02f, -7.356456667e-02f, -4.906767607e-02f, -2.454122901e-02f,
+    0.000000000e+00f, 2.454122901e-02f, 4.906767607e-02f, 7.356456667e-02f,
+    9.801714122e-02f, 1.224106774e-01f, 1.467304677e-01f, 1.709618866e-01f,
+    1.950903237e-01f, 2.191012353e-01f, 2.429801822e-01f, 2.667127550e-01f,
+    2.902846634e-01f, 3.136817515e-01f, 3.368898630e-01f, 3.598950505e-01f,
+    3.826834261e-01f, 4.052413106e-01f, 4.275550842e-01f, 4.496113360e-01f,
+    4.713967443e-01f, 4.928981960e-01f, 5.141027570e-01f, 5.349976420e-01f,
+    5.555702448e-01f, 5.758081675e-01f, 5.956993103e-01f, 6.152315736e-01f,
+    6.343932748e-01f, 6.531728506e-01f, 6.715589762e-01f, 6.895405650e-01f,
+    7.071067691e-01f, 7.242470980e-01f, 7.409511209e-01f, 7.572088242e-01f,
+    7.730104327e-01f, 7.883464098e-01f, 8.032075167e-01f, 8.175848126e-01f,
+    8.314695954e-01f, 8.448535800e-01f, 8.577286005e-01f, 8.700869679e-01f,
+    8.819212914e-01f, 8.932242990e-01f, 9.039893150e-01f, 9.142097831e-01f,
+    9.238795042e-01f, 9.329928160e-01f, 9.415440559e-01f, 9.495281577e-01f,
+    9.569403529e-01f, 9.637760520e-01f, 9.700312614e-01f, 9.757021070e-01f,
+    9.807852507e-01f, 9.852776527e-01f, 9.891765118e-01f, 9.924795628e-01f,
+    9.951847196e-01f, 9.972904325e-01f, 9.987954497e-01f, 9.996988177e-01f};
+__device__ __forceinline__ void tw16_fill(cf *tw16, int tid, int nthreads) {
+    for (int i = tid; i < 256; i += nthreads) {
+        const int k = i >> 4, q = i & 15, m = k * q;             // m < 256
+        tw16[k * kTw16Pitch + q] = make_float2(kCos256[m], -kCos256[(m + 192) & 255]);
+    }
+}
+
 template <int L, int BATCH, int T, bool WAVE = false, int XRS = 1>
 struct Fft {
     using LD = Lds<L, XRS>;
@@ -209,6 +292,19 @@ struct Fft {
     // Run the stage list.  Ns = product of the radices already applied.
     template <bool INV, int Ns, int R, int... Rest>
     __device__ static __forceinline__ void run(cf (&v)[E], cf *lds, int tid) {
+        run_impl<INV, false, Ns, R, Rest...>(v, lds, tid, nullptr);
+    }
+    // The same with the radix-16 stage after a radix-16 stage (Ns = 16: the
+    // 15 twiddles w^q, w = e^{-+2 pi i k/256}, k < 16) read from the table
+    // tw16[k * kTw16Pitch + q] = e^{-2 pi i k q / 256} (tw16_fill) instead of
+    // 4 native sincos + 11 products per butterfly.
+    template <bool INV, int Ns, int R, int... Rest>
+    __device__ static __forceinline__ void run_tw(cf (&v)[E], cf *lds, int tid, const cf *tw16) {
+        run_impl<INV, PSS_TW16 != 0, Ns, R, Rest...>(v, lds, tid, tw16);
+    }
+
+    template <bool INV, bool TW, int Ns, int R, int... Rest>
+    __device__ static __forceinline__ void run_impl(cf (&v)[E], cf *lds, int tid, const cf *tw16) {
         static_assert(E % R == 0, "E must be a multiple of every radix");
         constexpr int LR = L / R;
 #pragma unroll
@@ -216,7 +312,11 @@ struct Fft {
             const int j = tid + ib * T, b = j / LR, jj = j - b * LR;
             const int k = jj % Ns;
             cf *a = v + ib * R;
-            if constexpr (Ns > 1) {
+            if constexpr (TW && Ns == 16 && R == 16) {
+                const cf *t = tw16 + k * kTw16Pitch;
+#pragma unroll
+                for (int q = 1; q < 16; ++q) a[q] = INV ? cmul_conj(a[q], t[q]) : cmul(a[q], t[q]);
+            } else if constexpr (Ns > 1) {
                 // a[q] *= w^q, w = exp(-+2 pi i k / (Ns R)).  w^(2^j) from the
                 // native trig (angles < 1/2 rev), the other powers as products
                 // of at most four of those (<= 3 roundings).
@@ -262,7 +362,7 @@ struct Fft {
             constexpr int R2 = first<Rest...>();
             load<R2>(v, lds, tid);
             stage_sync<WAVE>();
-            run<INV, Ns * R, Rest...>(v, lds, tid);
+            run_impl<INV, TW, Ns * R, Rest...>(v, lds, tid, tw16);
         }
     }
 

@@ -1207,7 +1207,9 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
     template <bool MASK, bool TAIL = false>
     __device__ static void pass(const KP &k) {
         __shared__ cf lds[2 * Lds<N2>::RS];
+        __shared__ cf tw16[kTw16Size];
         const int tid = threadIdx.x;
+        tw16_fill(tw16, tid, T);     // first read after the first stage's barrier
         const int pr = blockIdx.x;                 // channel pair
         const int j = blockIdx.y;                  // row pair {j, N1-j}; {0, N1/2}
         const int N1 = (int)k.N1;
@@ -1232,7 +1234,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
 #pragma unroll
                 for (int q = 0; q < RF0; ++q) v[ib * RF0 + q] = Y.ld2(off, q * kQS);
             }
-            if constexpr (!(kAbl & 2)) FF::template run<false, 1, F...>(v, lds, tid);
+            if constexpr (!(kAbl & 2)) FF::template run_tw<false, 1, F...>(v, lds, tid, tw16);
             FF::template store<RFL>(v, lds, tid);
             __syncthreads();
 #pragma unroll
@@ -1279,7 +1281,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                 }
             }
             __syncthreads();
-            if constexpr (!(kAbl & 2)) FF::template run<true, 1, I...>(v, lds, tid);
+            if constexpr (!(kAbl & 2)) FF::template run_tw<true, 1, I...>(v, lds, tid, tw16);
 #pragma unroll
             for (int ib = 0; ib < E / RF0; ++ib) {
                 const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
@@ -1315,7 +1317,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                 }
             }
             __syncthreads();
-            if constexpr (!(kAbl & 2)) FF::template run<true, 1, I...>(v, lds, tid);
+            if constexpr (!(kAbl & 2)) FF::template run_tw<true, 1, I...>(v, lds, tid, tw16);
 #pragma unroll
             for (int ib = 0; ib < E / RF0; ++ib) {
                 const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
@@ -1364,7 +1366,9 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     template <bool FAST, bool SHARED = false>
     __device__ static void passA(const KP &k) {
         __shared__ cf lds[B * LdsC::RS];
+        __shared__ cf tw16[kTw16Size];
         const int tid = threadIdx.x;
+        tw16_fill(tw16, tid, T);     // read after the generate loop's barrier
         int cbx, pr;
         xcd_block(cbx, pr);
         const int ra = 2 * pr - k.poff, rb = ra + 1;
@@ -1491,7 +1495,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             cf *wl = lds + wv * LdsC::RS;
             FW::template load<RF0>(v, wl, lane);
             stage_sync<true>();
-            if constexpr (!(kAbl & 2)) FW::template run<false, 1, F...>(v, wl, lane);
+            if constexpr (!(kAbl & 2)) FW::template run_tw<false, 1, F...>(v, wl, lane, tw16);
 #pragma unroll
             for (int i = 0; i < E; ++i) {
                 int b0, k1;
@@ -1505,7 +1509,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         } else {
             FF::template load<RF0>(v, lds, tid);
             __syncthreads();
-            if constexpr (!(kAbl & 2)) FF::template run<false, 1, F...>(v, lds, tid);
+            if constexpr (!(kAbl & 2)) FF::template run_tw<false, 1, F...>(v, lds, tid, tw16);
 #pragma unroll
             for (int i = 0; i < E; ++i) {
                 int b, k1;
@@ -1564,6 +1568,8 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     // half-line reads / 32-B output segments of neighbouring blocks stop
     // merging (PMC: +19% FETCH, +31% WRITE, pass C 17.6 -> 18.5 ms).
     __device__ static __forceinline__ void inv_block(const KP &k, const cf *Yp, int64_t n20, cf *lds, int tid) {
+        __shared__ cf tw16[kTw16Size];
+        tw16_fill(tw16, tid, T);     // read after the spill loads' barrier
         const int64_t N2 = k.N2;
         const float invN = k.invN;
         const Buf Y(Yp, (uint32_t)(pstride(k) * 8));   // one pair spill, < 2^28 bytes
@@ -1633,12 +1639,12 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             cf *wl = lds + wv * LdsC::RS;
             FW::template load<RI0>(v, wl, lane);
             stage_sync<true>();
-            if constexpr (!(kAbl & 2)) FW::template run<true, 1, I...>(v, wl, lane);
+            if constexpr (!(kAbl & 2)) FW::template run_tw<true, 1, I...>(v, wl, lane, tw16);
             FW::template store<RIL>(v, wl, lane);
         } else {
             FF::template load<RI0>(v, lds, tid);
             __syncthreads();
-            if constexpr (!(kAbl & 2)) FF::template run<true, 1, I...>(v, lds, tid);
+            if constexpr (!(kAbl & 2)) FF::template run_tw<true, 1, I...>(v, lds, tid, tw16);
             FF::template store<RIL>(v, lds, tid);
         }
         __syncthreads();
