@@ -194,7 +194,7 @@ struct KP {
     int log2n;
     const uint2 *mt_bits;   // [N/32] {nulled-for-every-f bits, f-dependent bits}
     const uint32_t *mt_base;// [N/32] index of the word's first f-dependent position
-    const float *mt_coef;   // [n_f_dependent][KCH] Chebyshev coefficients in t
+    const float *mt_coef;   // [n_f_dependent][KCH] root records of the f-dependent positions (root_hit)
     const uint32_t *mbits;  // [nchan][N/32] per-channel null decisions (k_mask_bits)
     int mbB;                // column-block width B of pass C (mbits layout)
     const cf *rtab;         // [nchan][RFL] row-pass ramp factors (k_ramp_tab)
@@ -223,7 +223,9 @@ __host__ __device__ __forceinline__ int64_t pstride(const KP &k) { return k.N1 *
 // from KCH = 12 node shifts is exact to ~1e-9 relative (tools: DESIGN.md §3).
 // Per position the table stores whether M > 1 for EVERY f (bound
 // c0 -+ sum|c_n|), for NO f, or -- for the ~2% of positions near box edges
-// where the answer depends on f -- the 12 coefficients.  The node shifts are
+// where the answer depends on f -- the f values (as t) where the fp32
+// interpolant crosses 1, found once per position by the table build
+// (root_hit; the per-channel lookup is then two compares).  The node shifts are
 // KCH/2 pair rows through the same FFT engine, once per run; per channel
 // nothing but a table lookup remains (no per-channel mask FFT or spill).
 // ---------------------------------------------------------------------------
@@ -239,13 +241,8 @@ __device__ __forceinline__ void mask_split(uint64_t w, int L, uint32_t &ishift, 
     t = fmaf((float)(uint32_t)(fr >> 40), 1.1920928955078125e-07f, -1.0f);   // 2 f - 1
 }
 
-__device__ __forceinline__ float cheb_eval_r(const float4 (&q)[3], float t);
-__device__ __forceinline__ float cheb_eval(const float *c, float t) {
-    const float4 q[3] = {reinterpret_cast<const float4 *>(c)[0], reinterpret_cast<const float4 *>(c)[1],
-                         reinterpret_cast<const float4 *>(c)[2]};
-    return cheb_eval_r(q, t);
-}
-// the same Clenshaw evaluation from coefficients already in registers
+// Clenshaw evaluation of the degree-11 Chebyshev interpolant at t (the mask
+// value M(p, f), t = 2 f - 1), fp32: the table build's root scan uses it
 __device__ __forceinline__ float cheb_eval_r(const float4 (&q)[3], float t) {
     const float4 a = q[0], b = q[1], d = q[2];
     const float cc[KCH] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, d.x, d.y, d.z, d.w};
@@ -258,6 +255,23 @@ __device__ __forceinline__ float cheb_eval_r(const float4 (&q)[3], float t) {
         b1 = b0;
     }
     return fmaf(t, b1, cc[0] - b2);
+}
+
+// Decision of an f-dependent position from its ROOT record (k_mask_table):
+// rec = {count, s0, r_1 .. r_10}: the fp32 Chebyshev value at t exceeds 1
+// iff s0 XOR (the number of roots r_i < t) is odd.  The roots are where
+// cheb_eval_r(c, .) > 1 flips (33-point scan of t in [-1, 1], 24 bisection
+// steps each), so the rule reproduces the direct evaluation except within
+// ~1e-8 of a flip, with one 16-B load and two compares per position instead
+// of 48 B of coefficients and a 12-term Clenshaw sum; unused roots are +inf.
+// `a` is the record's first float4.
+__device__ __forceinline__ bool root_hit(const float4 a, const float *rec, float t) {
+    bool h = (a.y != 0.f) ^ (t > a.z) ^ (t > a.w);
+    if (a.x > 2.f) {                    // rare: more than two flips over f in [0, 1)
+        const float4 b = reinterpret_cast<const float4 *>(rec)[1], c = reinterpret_cast<const float4 *>(rec)[2];
+        h ^= (t > b.x) ^ (t > b.y) ^ (t > b.z) ^ (t > b.w) ^ (t > c.x) ^ (t > c.y) ^ (t > c.z) ^ (t > c.w);
+    }
+    return h;
 }
 
 // Null decision bits (bit i: sample n0 + i) for 4 consecutive samples of a
@@ -278,7 +292,8 @@ __device__ __forceinline__ uint32_t mask_hits4(const KP &k, int64_t n0, uint32_t
                 const uint32_t p = (p0 + (uint32_t)i) & nm, pw = p >> 5;
                 const uint32_t word = (pw == w) ? A.y : Bw.y;
                 const uint32_t idx = k.mt_base[pw] + (uint32_t)__popc(word & ((1u << (p & 31u)) - 1u));
-                const bool hit = cheb_eval(k.mt_coef + (int64_t)idx * KCH, t) > 1.0f;
+                const float *rec = k.mt_coef + (int64_t)idx * KCH;
+                const bool hit = root_hit(reinterpret_cast<const float4 *>(rec)[0], rec, t);
                 r = (r & ~(1u << i)) | ((uint32_t)hit << i);
             }
         }
@@ -296,7 +311,7 @@ __device__ __forceinline__ uint32_t mask_run(const KP &k, uint32_t n, uint32_t i
     const uint32_t msk = RUN >= 32u ? 0xffffffffu : ((1u << RUN) - 1u);
     uint32_t r32 = (uint32_t)(((((uint64_t)Bw.x) << 32) | A.x) >> sh) & msk;
     uint32_t amb = (uint32_t)(((((uint64_t)Bw.y) << 32) | A.y) >> sh) & msk;
-    if (!amb) return r32;
+    if (!amb || (kAbl & 256)) return r32;       // (ablation 256: no f-dependent evaluations)
     // Ambiguous positions cluster at pulse edges (a lane may hold ~20): take
     // them four at a time so the coefficient loads of a group are in flight
     // together instead of one exposed latency per position (the table bases
@@ -313,18 +328,17 @@ __device__ __forceinline__ uint32_t mask_run(const KP &k, uint32_t n, uint32_t i
             const uint32_t word = inA ? A.y : Bw.y;
             idx[u] = (inA ? baseA : baseB) + (uint32_t)__popc(word & ((1u << (p & 31u)) - 1u));
         }
-        float4 c[4][3];
+        float4 a[4];
+        const float *rec[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const float4 *q = reinterpret_cast<const float4 *>(k.mt_coef + (int64_t)(ii[u] < 32u ? idx[u] : idx[0]) * KCH);
-            c[u][0] = q[0];
-            c[u][1] = q[1];
-            c[u][2] = q[2];
+            rec[u] = k.mt_coef + (int64_t)(ii[u] < 32u ? idx[u] : idx[0]) * KCH;
+            a[u] = reinterpret_cast<const float4 *>(rec[u])[0];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (ii[u] < 32u) {
-                const bool hit = cheb_eval_r(c[u], t) > 1.0f;
+                const bool hit = root_hit(a[u], rec[u], t);
                 r32 = (r32 & ~(1u << ii[u])) | ((uint32_t)hit << ii[u]);
             }
         }
@@ -1873,11 +1887,37 @@ __global__ __launch_bounds__(256) void k_mask_table(const float *nodes, int64_t 
         base[(p >> 5) + 1] = b0 + (uint32_t)__popc((uint32_t)ab);
     }
     if (amb) {
+        // root record (root_hit): where the fp32 Clenshaw value crosses 1
+        const float4 q[3] = {make_float4(c[0], c[1], c[2], c[3]), make_float4(c[4], c[5], c[6], c[7]),
+                             make_float4(c[8], c[9], c[10], c[11])};
+        float rt[10];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) rt[i] = INFINITY;
+        bool prev = cheb_eval_r(q, -1.0f) > 1.0f;
+        const bool s0 = prev;
+        int cnt = 0;
+        float tprev = -1.0f;
+        for (int jg = 1; jg <= 32; ++jg) {
+            const float tg = -1.0f + (float)jg * 0.0625f;
+            const bool cur = cheb_eval_r(q, tg) > 1.0f;
+            if (cur != prev) {
+                float lo = tprev, hi = tg;            // decision prev at lo, cur at hi
+                for (int it = 0; it < 24; ++it) {
+                    const float mid = 0.5f * (lo + hi);
+                    if ((cheb_eval_r(q, mid) > 1.0f) == prev) lo = mid; else hi = mid;
+                }
+#pragma unroll
+                for (int i = 0; i < 10; ++i) if (i == cnt) rt[i] = lo;
+                ++cnt;
+            }
+            prev = cur;
+            tprev = tg;
+        }
         const uint32_t idx = b0 + (uint32_t)__popcll(ab & ((1ull << lane) - 1ull));
         float4 *dst = reinterpret_cast<float4 *>(coef + (int64_t)idx * KCH);
-        dst[0] = make_float4(c[0], c[1], c[2], c[3]);
-        dst[1] = make_float4(c[4], c[5], c[6], c[7]);
-        dst[2] = make_float4(c[8], c[9], c[10], c[11]);
+        dst[0] = make_float4((float)min(cnt, 10), s0 ? 1.0f : 0.0f, rt[0], rt[1]);
+        dst[1] = make_float4(rt[2], rt[3], rt[4], rt[5]);
+        dst[2] = make_float4(rt[6], rt[7], rt[8], rt[9]);
     }
 }
 
