@@ -360,7 +360,7 @@ def main():
                     help="weak: --nchan channels per GPU; strong: --nchan channels in total, split over the GPUs")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU-only check of the launcher / JSON contract: host planning only, gloo, no GPU")
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--nchan", type=int, default=NCHAN, help="channels per GPU")
     ap.add_argument("--log2n", type=int, default=LOG2N)
