@@ -31,7 +31,11 @@ the timing barrier and the max-over-ranks reduction are the only RCCL calls
 
 Reports (one JSON line on rank 0): value = channel-samples/s over all ranks,
 the roofline of the dominant kernel (HIP events on the launch stream, inside
-the timed region), and the CPU oracle timed on a bounded channel sample.
+the timed region), and the CPU oracle timed on a bounded channel sample; next
+to them the first and steady step spans (step_ms_first / step_ms_steady: the
+first timed step starts on an idle GPU and carries its host planning) and the
+GPU's socket power and gfx clock through the timed steps (gpu_power).
+Defaults: 20 timed steps after 2 warm-up steps, N = 1.
 """
 import argparse
 import contextlib
