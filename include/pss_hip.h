@@ -15,7 +15,7 @@
  *  - Return codes: PSS_OK = 0, PSS_EINVAL = -1 (-> ValueError),
  *    PSS_EUNSUPPORTED = -2 (-> NotImplementedError), PSS_EHIP = -3
  *    (-> RuntimeError); pss_last_error() returns the message.
- *  - Randomness is counter-based Philox4x32-10 keyed by (seed, call id,
+ *  - Randomness is counter-based Philox4x32-7 keyed by (seed, call id,
  *    purpose, GLOBAL channel, sample): results do not depend on how channels
  *    are split across launches or GPUs.
  */

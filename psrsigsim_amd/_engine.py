@@ -412,7 +412,12 @@ def check_null_status(sig):
     """Raise the reference's error for a null() whose channel-0 maximum was
     not unique (pulsar.py:286-288: the broadcast of a shift_val of size != 1
     fails).  Deferred to the first read of the data: the value is on the
-    device, and reading it at null() time would stall the host."""
+    device, and reading it at null() time would stall the host.  A failed
+    check is sticky: the data then holds a null the reference never made, so
+    every later read-out raises the same error (not only the first)."""
+    err = getattr(sig, "_null_error", None)
+    if err is not None:
+        raise ValueError(err)
     checks = getattr(sig, "_null_checks", None)
     if not checks:
         return
@@ -420,7 +425,8 @@ def check_null_status(sig):
     for t, nph in checks:
         st = int(t[1].item())
         if st != 0:
-            raise ValueError("operands could not be broadcast together with shapes (%d,) (%s,)"
-                             % (nph, "0" if st == 2 else "2+"))
+            sig._null_error = ("operands could not be broadcast together with shapes (%d,) (%s,)"
+                               % (nph, "0" if st == 2 else "2+"))
+            raise ValueError(sig._null_error)
 
 

@@ -1,5 +1,5 @@
 // pss_device.hpp -- gfx950 device helpers: complex arithmetic, revolution-based
-// native trig, fixed-point phases, Philox4x32-10 and chi-square samplers.
+// native trig, fixed-point phases, Philox4x32-7 and chi-square samplers.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -52,6 +52,11 @@ __device__ __forceinline__ cf expi_rev(float r) {
 __device__ __forceinline__ float fix_to_rev(uint64_t ph) {
     int32_t hi = (int32_t)(uint32_t)(ph >> 32);   // top 32 bits, signed
     return (float)hi * 2.3283064365386963e-10f;   // * 2^-32
+}
+
+// 2^-32-cycle fixed point phase -> signed revolutions in [-0.5, 0.5).
+__device__ __forceinline__ float fix32_to_rev(uint32_t ph) {
+    return (float)(int32_t)ph * 2.3283064365386963e-10f;   // * 2^-32
 }
 
 // --------------------------------------------------------------------------
@@ -107,10 +112,14 @@ struct Buf {
 };
 
 // --------------------------------------------------------------------------
-// Philox4x32-10 (Salmon et al., SC'11)
+// Philox4x32-7 (Salmon et al., SC'11).  7 rounds is the round count the
+// Random123 paper reports as passing BigCrush for Philox4x32 (10 is its
+// default safety margin).  The step is power-throttled and issue-bound, so the
+// 3 rounds (12 VALU per 4 draws) are worth 0.9 ms at C3; the distribution
+// gates (KS / moments, tests/test_gpu_stats.py) guard the generator.
 // --------------------------------------------------------------------------
 #ifndef PSS_PHILOX_ROUNDS
-#define PSS_PHILOX_ROUNDS 10
+#define PSS_PHILOX_ROUNDS 7
 #endif
 __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll

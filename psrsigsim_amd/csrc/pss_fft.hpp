@@ -292,7 +292,7 @@ struct Fft {
     // Run the stage list.  Ns = product of the radices already applied.
     template <bool INV, int Ns, int R, int... Rest>
     __device__ static __forceinline__ void run(cf (&v)[E], cf *lds, int tid) {
-        run_impl<INV, false, Ns, R, Rest...>(v, lds, tid, nullptr);
+        run_impl<INV, false, false, Ns, R, Rest...>(v, lds, tid, nullptr);
     }
     // The same with the radix-16 stage after a radix-16 stage (Ns = 16: the
     // 15 twiddles w^q, w = e^{-+2 pi i k/256}, k < 16) read from the table
@@ -300,10 +300,19 @@ struct Fft {
     // 4 native sincos + 11 products per butterfly.
     template <bool INV, int Ns, int R, int... Rest>
     __device__ static __forceinline__ void run_tw(cf (&v)[E], cf *lds, int tid, const cf *tw16) {
-        run_impl<INV, PSS_TW16 != 0, Ns, R, Rest...>(v, lds, tid, tw16);
+        run_impl<INV, PSS_TW16 != 0, false, Ns, R, Rest...>(v, lds, tid, tw16);
     }
 
-    template <bool INV, bool TW, int Ns, int R, int... Rest>
+    // Every stage but the last, then the exchange into the last stage's input
+    // mapping: the caller runs the last stage itself (pass A merges the
+    // four-step twiddle into it).  Ns of the last stage = L / (its radix).
+    template <bool INV, int Ns, int R, int... Rest>
+    __device__ static __forceinline__ void run_head_tw(cf (&v)[E], cf *lds, int tid, const cf *tw16) {
+        static_assert(sizeof...(Rest) >= 1, "run_head_tw needs at least two stages");
+        run_impl<INV, PSS_TW16 != 0, true, Ns, R, Rest...>(v, lds, tid, tw16);
+    }
+
+    template <bool INV, bool TW, bool HEAD, int Ns, int R, int... Rest>
     __device__ static __forceinline__ void run_impl(cf (&v)[E], cf *lds, int tid, const cf *tw16) {
         static_assert(E % R == 0, "E must be a multiple of every radix");
         constexpr int LR = L / R;
@@ -362,7 +371,7 @@ struct Fft {
             constexpr int R2 = first<Rest...>();
             load<R2>(v, lds, tid);
             stage_sync<WAVE>();
-            run_impl<INV, TW, Ns * R, Rest...>(v, lds, tid, tw16);
+            if constexpr (!(HEAD && sizeof...(Rest) == 1)) run_impl<INV, TW, HEAD, Ns * R, Rest...>(v, lds, tid, tw16);
         }
     }
 

@@ -57,6 +57,11 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 #ifndef PSS_WAVE_COLS
 #define PSS_WAVE_COLS 1
 #endif
+// pass A: the four-step twiddle folded into the last column-FFT stage (1) or
+// applied after the FFT (0); experiment switch
+#ifndef PSS_MERGE_TW
+#define PSS_MERGE_TW 1
+#endif
 // delayed-null fix-up over the list of table words with nulls (1) or over
 // every word of every channel (0); experiment switch
 #ifndef PSS_NULL_LIST
@@ -197,7 +202,7 @@ struct KP {
     const float *mt_coef;   // [n_f_dependent][KCH] root records of the f-dependent positions (root_hit)
     const uint32_t *mbits;  // [nchan][N/32] per-channel null decisions (k_mask_bits)
     int mbB;                // column-block width B of pass C (mbits layout)
-    const cf *rtab;         // [nchan][RFL] row-pass ramp factors (k_ramp_tab)
+    const cf *rtab;         // [npairs][RFL][2] row-pass pair ramp factors {E, D} (k_pair_tab)
     hipEvent_t after_a;     // batching: recorded after this launch's pass A (or NULL)
     hipEvent_t mask_ready;  // mask table built on a side stream: wait before its first use (or NULL)
     const uint32_t *wlist;  // delayed null: table words with a nulled position (any f)
@@ -643,6 +648,13 @@ struct PhaseWalk {
             u += (float)(iv - (uint32_t)(p.nint - 1));
             iv = p.nint - 1;
         }
+    }
+    // the same for a table that spans the whole period (nint == knot_m, the
+    // host's extrapolated pieces appended: pulsar._device_table), where
+    // iv < knot_m needs no clamp -- bitwise what get() returns then
+    __device__ __forceinline__ void get_full(uint32_t &iv, float &u) const {
+        iv = (uint32_t)(u64 >> 32);
+        u = frac23((uint32_t)u64);
     }
 };
 __device__ __forceinline__ void phase_delta(const PssPipeline &p, uint32_t &dlo, uint64_t &dhi) {
@@ -1177,21 +1189,36 @@ __device__ __forceinline__ cf ramp_q(uint64_t p0, uint64_t step, uint64_t nw, in
     return expi_rev(-fix_to_rev(ph));
 }
 
-// Per-channel factors of the row-pass ramps: bin kb0 + q N/RFL has phase
-// p0 + q (N/RFL) w - [2q >= RFL] N w; the q-dependent part is the same for every
-// thread, so it is tabulated once per run (double precision, with the 1/2 of
-// the Hermitian separation folded in) and a bin's ramp is base(kb0) * tab[q].
+// Pair form of the ramps.  With R_a = e^{-2 pi i k' w_a / 2^64} and R_b the
+// two channels' ramps, the recombined bin W = D_a R_a + i D_b R_b of the pair
+// row (D_a = (Z + conj Zm)/2, D_b = (Z - conj Zm)/2i) is
+//     W = E (Z cos d - i conj(Zm) sin d),   E = e^{-i (alpha + beta)/2},
+//                                           d = (alpha - beta)/2,
+// because (R_a + R_b)/2 = E cos d and (R_a - R_b)/2 = -i E sin d.  E and
+// D = e^{-i d} come from the half words h = w >> 1 (h_a + h_b and h_a - h_b):
+// any h with 2h = w mod 2^64 gives the same W (a dropped top bit flips E and
+// D together by (-1)^k'), so no extra host data is needed.  Per bin that is
+// two complex products for E and D (base(kb0) x table[q], as before) plus
+// four products and one complex product for W: 16 VALU instead of 22.
+// Per-pair factors: bin kb0 + q N/RFL has phase offset q (N/RFL) h - [2q >=
+// RFL] N h relative to kb0; tabulated once per run in double precision,
+// tab[pair][q] = {E factor, D factor}.
 template <int RFL>
-__global__ void k_ramp_tab(const uint64_t *ramp, int64_t N, int nchan, cf *tab) {
-    const int r = blockIdx.x, q = threadIdx.x;
-    if (r >= nchan || q >= RFL) return;
-    const uint64_t w = (uint64_t)ramp[r];
-    uint64_t ph = (uint64_t)q * ((uint64_t)(N / RFL) * w);
-    if (2 * q >= RFL) ph -= (uint64_t)N * w;
-    const double rev = (double)(int64_t)ph * 5.421010862427522e-20;   // 2^-64
-    double sn, cs;
-    sincospi(2.0 * rev, &sn, &cs);
-    tab[(int64_t)r * RFL + q] = make_float2((float)(0.5 * cs), (float)(-0.5 * sn));
+__global__ void k_pair_tab(const uint64_t *ramp, int64_t N, int nchan, int poff, int npairs, cf *tab) {
+    const int pr = blockIdx.x, q = threadIdx.x;
+    if (pr >= npairs || q >= RFL) return;
+    const int ra = max(2 * pr - poff, 0), rb = min(2 * pr + 1 - poff, nchan - 1);
+    const uint64_t ha = (uint64_t)ramp[ra] >> 1, hb = (uint64_t)ramp[rb] >> 1;
+    const uint64_t h2[2] = {ha + hb, ha - hb};
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        uint64_t ph = (uint64_t)q * ((uint64_t)(N / RFL) * h2[e]);
+        if (2 * q >= RFL) ph -= (uint64_t)N * h2[e];
+        const double rev = (double)(int64_t)ph * 5.421010862427522e-20;   // 2^-64
+        double sn, cs;
+        sincospi(2.0 * rev, &sn, &cs);
+        tab[((int64_t)pr * RFL + q) * 2 + e] = make_float2((float)cs, (float)(-sn));
+    }
 }
 
 template <int N2, int T, typename FWD, typename INV>
@@ -1251,13 +1278,16 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
             if constexpr (!(kAbl & 2)) FF::template run_tw<false, 1, F...>(v, lds, tid, tw16);
             FF::template store<RFL>(v, lds, tid);
             __syncthreads();
+            // pair ramp factors (k_pair_tab): {E, D} per q, wave-uniform
+            const cf *ptab = k.rtab + (int64_t)pr * (2 * RFL);
+            const uint64_t hsum = (rwa >> 1) + (rwb >> 1), hdif = (rwa >> 1) - (rwb >> 1);
 #pragma unroll
             for (int ib = 0; ib < E / RFL; ++ib) {
                 const int jg = tid + ib * T, b = jg / LRL, jj = jg - b * LRL;
                 const int row = b ? rowB : rowA;
                 const int64_t kb0 = row + (int64_t)N1 * jj;
-                const uint64_t p0a = (uint64_t)kb0 * rwa, p0b = (uint64_t)kb0 * rwb;
-                const cf ba = expi_rev(-fix_to_rev(p0a)), bb = expi_rev(-fix_to_rev(p0b));
+                const cf bE = expi_rev(-fix_to_rev((uint64_t)kb0 * hsum));
+                const cf bD = expi_rev(-fix_to_rev((uint64_t)kb0 * hdif));
 #pragma unroll
                 for (int q = 0; q < RFL; ++q) {
                     const int i = ib * RFL + q, k2 = jj + q * LRL;
@@ -1265,7 +1295,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                     if (j == 0) { bm = b; k2m = (row == 0) ? ((N2 - k2) & (N2 - 1)) : (N2 - 1 - k2); }
                     else        { bm = 1 - b; k2m = N2 - 1 - k2; }
                     const cf Z = v[i], Zm = lds[Lds<N2>::at(bm, k2m)];
-                    // 2 D_a and 2 D_b (the 1/2 is folded into the ramp table)
+                    // 2 D_a and 2 D_b (DC / Nyquist and the tail extension)
                     const cf Sa = make_float2(Z.x + Zm.x, Z.y - Zm.y);
                     const cf Sb = make_float2(Z.y + Zm.y, Zm.x - Z.x);
                     if constexpr (kAbl & 8) {
@@ -1282,15 +1312,21 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                         const cf Da = make_float2(0.5f * Sa.x, 0.5f * Sa.y), Db = make_float2(0.5f * Sb.x, 0.5f * Sb.y);
                         v[i] = make_float2(Da.x - Db.y, Da.y + Db.x);
                     } else {
-                        cf ra_ = cmul(ba, k.rtab[(int64_t)ra * RFL + q]), rb_ = cmul(bb, k.rtab[(int64_t)rb * RFL + q]);
+                        const cf Ef = cmul(bE, ptab[2 * q]), Df = cmul(bD, ptab[2 * q + 1]);
                         if constexpr (TAIL) {
+                            // per-channel transfer functions: R_a = E D, R_b = E conj(D)
                             const cf w = bin_phasor(kb0 + (int64_t)q * (k.N / RFL), k.N);
-                            ra_ = cmul(ra_, tail_factor(k.p.tail_a[ra], w));
-                            rb_ = cmul(rb_, tail_factor(k.p.tail_a[rb], w));
+                            const cf ra_ = cmul(make_float2(0.5f * Ef.x, 0.5f * Ef.y), cmul(Df, tail_factor(k.p.tail_a[ra], w)));
+                            const cf rb_ = cmul(make_float2(0.5f * Ef.x, 0.5f * Ef.y), cmul_conj(tail_factor(k.p.tail_a[rb], w), Df));
+                            const cf A = cmul(Sa, ra_);
+                            const cf Bv = cmul(Sb, rb_);
+                            v[i] = make_float2(A.x - Bv.y, A.y + Bv.x);
+                        } else {
+                            // W = E (Z cos d - i conj(Zm) sin d), D = cos d - i sin d
+                            const float c = Df.x, s = -Df.y;
+                            const cf in = make_float2(fmaf(Z.x, c, -(Zm.y * s)), fmaf(Z.y, c, -(Zm.x * s)));
+                            v[i] = cmul(Ef, in);
                         }
-                        const cf A = cmul(Sa, ra_);
-                        const cf Bv = cmul(Sb, rb_);
-                        v[i] = make_float2(A.x - Bv.y, A.y + Bv.x);
                     }
                 }
             }
@@ -1364,6 +1400,8 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     // only the transposes between sample-major items and columns need one.
     using FW = Fft<(N1 % 64 == 0 ? N1 : 64), 1, 64, true, XRS>;   // same row layout as LdsC (placeholder when N1 % 64 != 0)
     static constexpr bool kWaveCols = PSS_WAVE_COLS && (T == 64 * B) && (N1 % 64 == 0) && (N1 / 64 == E);
+    // pass A: four-step twiddle folded into the column FFT's last stage
+    static constexpr bool kMergeTw = PSS_MERGE_TW && sizeof...(F) >= 2;
     static constexpr int RF0 = FF::template first<F...>();
     static constexpr int RFL = FF::template last_of<F...>();
     static constexpr int RI0 = FF::template first<I...>();
@@ -1412,7 +1450,9 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                 if constexpr (!shared) ptab[1][i] = prof[(int64_t)rowb * nint + i];
             }
             __syncthreads();
-            const float dn = p.draw_norm;
+            // draw_norm, or 0 for a pair's missing channel (shard / band
+            // edges): the multiply the sample needs anyway zeroes it, no select
+            const float dna = hasa ? p.draw_norm : 0.f, dnb = hasb ? p.draw_norm : 0.f;
 #if PSS_PHASE_WALK
             uint32_t dlo;
             uint64_t dhi;
@@ -1448,7 +1488,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                     float u;
 #if PSS_PHASE_WALK
                     if (i) w.step(dlo, dhi, M);
-                    w.get(p, iv, u);
+                    w.get_full(iv, u);       // fast_source(): nint == knot_m
 #else
                     pchip_locate(k, (int64_t)(n + (uint32_t)i), iv, u);
 #endif
@@ -1459,8 +1499,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                         const float4 Bc = ptab[1][iv];
                         pb = fmaf(fmaf(fmaf(Bc.x, u, Bc.y), u, Bc.z), u, Bc.w);
                     }
-                    const float xa = pa * va[i] * dn, xb = pb * vb[i] * dn;
-                    lds[LdsC::at(b4 + i, n1)] = make_float2(hasa ? xa : 0.f, hasb ? xb : 0.f);
+                    lds[LdsC::at(b4 + i, n1)] = make_float2(pa * va[i] * dna, pb * vb[i] * dnb);
                 }
             }
         } else
@@ -1509,15 +1548,44 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             cf *wl = lds + wv * LdsC::RS;
             FW::template load<RF0>(v, wl, lane);
             stage_sync<true>();
-            if constexpr (!(kAbl & 2)) FW::template run_tw<false, 1, F...>(v, wl, lane, tw16);
+            if constexpr (kMergeTw && !(kAbl & 6)) {
+                // Last stage (radix RFL at Ns = N1/RFL) with the four-step
+                // twiddle folded in.  Output m of butterfly jj is k1 = jj +
+                // Ns m, and W_N^{n2 k1} = W_N^{n2 jj} W_N^{n2 Ns m}: the first
+                // factor is common to the butterfly, so it joins the stage's
+                // input twiddles W_N1^{jj q} (one phase per input,
+                // W_N^{jj (n2 + N2 q)}), the second is wave-uniform (one
+                // product per output).  Phases in exact 32-bit fixed point.
+                FW::template run_head_tw<false, 1, F...>(v, wl, lane, tw16);
+                constexpr int NsL = N1 / RFL;
+                constexpr int LG1 = __builtin_ctz((unsigned)N1);
+                const int LGN = __builtin_ctzll((unsigned long long)k.N);        // N = 2^LGN here
+                const uint32_t A = (uint32_t)(n20 + wv) << (32 - LGN);           // n2 / N (2^-32 rev)
+                cf U[RFL];
 #pragma unroll
-            for (int i = 0; i < E; ++i) {
-                int b0, k1;
-                FW::template where<RFL>(i, lane, b0, k1);
-                const uint32_t m = (uint32_t)(n20 + wv) * (uint32_t)k1;
-                float rev = (float)m * invN;
-                if (rev >= 0.5f) rev -= 1.0f;
-                if constexpr (!(kAbl & 4)) v[i] = cmul(v[i], expi_rev(-rev)); else v[i] = v[i];
+                for (int m = 1; m < RFL; ++m) U[m] = expi_rev(-fix32_to_rev(A * (uint32_t)(NsL * m)));
+#pragma unroll
+                for (int ib = 0; ib < E / RFL; ++ib) {
+                    const uint32_t jj = (uint32_t)(lane + 64 * ib);              // < NsL
+                    const uint32_t X0 = jj * A, S = jj << (32 - LG1);
+                    cf *a = v + ib * RFL;
+#pragma unroll
+                    for (int q = 0; q < RFL; ++q) a[q] = cmul(a[q], expi_rev(-fix32_to_rev(X0 + (uint32_t)q * S)));
+                    dft<RFL, false>(a);
+#pragma unroll
+                    for (int m = 1; m < RFL; ++m) a[m] = cmul(a[m], U[m]);
+                }
+            } else {
+                if constexpr (!(kAbl & 2)) FW::template run_tw<false, 1, F...>(v, wl, lane, tw16);
+#pragma unroll
+                for (int i = 0; i < E; ++i) {
+                    int b0, k1;
+                    FW::template where<RFL>(i, lane, b0, k1);
+                    const uint32_t m = (uint32_t)(n20 + wv) * (uint32_t)k1;
+                    float rev = (float)m * invN;
+                    if (rev >= 0.5f) rev -= 1.0f;
+                    if constexpr (!(kAbl & 4)) v[i] = cmul(v[i], expi_rev(-rev)); else v[i] = v[i];
+                }
             }
             FW::template store<RFL>(v, wl, lane);
         } else {
@@ -2487,7 +2555,7 @@ static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
         w.coef = o;  o += al256(N * KCH * 4);
         w.misc = o;  o += 256;
         w.mbits = o; o += al256((int64_t)nchan * (N / 8));   // per-channel null bits
-        w.rtab = o;  o += al256((int64_t)nchan * 64 * 8);     // row-pass ramp factors (RFL <= 64)
+        w.rtab = o;  o += al256(npairs * 2 * 64 * 8);          // row-pass pair ramp factors (RFL <= 64)
         w.wlist = o; o += al256((N / 32) * 4);                 // null fix-up: table words with nulls
     } else if (filt || !(is_pow2(N) && N >= 64 && N <= 8192)) {
         // fallback: W1, W2, twiddles -- Bluestein needs W1 only (its forward
@@ -2525,8 +2593,10 @@ static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
 
 static bool fast_source(const PssPipeline &p) {
     if (g_flags & PSS_FLAG_NO_FAST) return false;
+    // (nint == knot_m: the table spans the period, so the fast walk needs no
+    // extrapolation clamp -- pulsar._device_table always builds it so)
     return p.src == PSS_SRC_SEARCH && !p.gen_amp && p.gen_df == 1.0f && !p.inj_gen && p.null_mode != PSS_NULL_UNDELAYED &&
-           p.nint <= kFastNint && !p.prof_split;
+           p.nint <= kFastNint && !p.prof_split && (uint32_t)p.nint == p.knot_m;
 }
 static bool fast_epilogue(const KP &k) {
     const PssPipeline &p = k.p;
@@ -2698,7 +2768,7 @@ static int launch_batches(KP &k, hipStream_t st, int nb) {
         kb.p.nyq_re = k.p.nyq_re + r0;
         kb.p.nyq_im = k.p.nyq_im + r0;
         if (k.p.mask_ramp) kb.p.mask_ramp = k.p.mask_ramp + r0;
-        kb.rtab = k.rtab + (int64_t)r0 * PR::RFL;
+        kb.rtab = k.rtab + (int64_t)p0 * 2 * PR::RFL;
         kb.Yd = k.Yd + (int64_t)p0 * pstride(k);
         kb.after_a = ss->ev[1 + b];
         hipStream_t sb = ss->s[b & 1];
@@ -2765,7 +2835,8 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
     }
     {
         cf *rt = reinterpret_cast<cf *>(w + L.rtab);
-        k_ramp_tab<PR::RFL><<<dim3((unsigned)k.p.nchan), dim3(64), 0, st>>>(k.p.ramp, k.N, k.p.nchan, rt);
+        k_pair_tab<PR::RFL><<<dim3((unsigned)k.npairs), dim3(64), 0, st>>>(k.p.ramp, k.N, k.p.nchan, k.poff,
+                                                                          k.npairs, rt);
         LAUNCHCHK();
         k.rtab = rt;
     }

@@ -253,11 +253,31 @@ class Pulsar(object):
 
 def _device_table(portrait):
     """(table, M, nint, split): uniform knots -> split None; non-uniform
-    knots -> the split-cell table (DataPortrait.split_table), nint = M."""
+    knots -> the split-cell table (DataPortrait.split_table), nint = M.
+
+    The device table always covers the whole period (nint == M): when the
+    knots stop short of phase 1 (arange(N)/N, portraits.py:231-240) the
+    reference extrapolates with the last piece (scipy's default), so the
+    intervals k = nint .. M-1 get that cubic re-expanded in their own local
+    coordinate, c(u + m) with m = k - nint + 1, in float64.  The kernels then
+    need no extrapolation branch per sample."""
     tab, M, third = portrait.device_table()
     if np.ndim(third) == 1:
         return tab, M, M, np.asarray(third, dtype=np.float32)
-    return tab, M, third, None
+    nint = int(third)
+    if nint < M:
+        from .portraits import rows_of
+        h = 1.0 / M
+        amax = portrait.Amax if hasattr(portrait, '_Amax') else 1.0
+        c = np.asarray(rows_of(portrait._coef), dtype=np.float64)[:, nint - 1, :]
+        d3, d2, d1, d0 = (c[:, 0] * h ** 3 / amax, c[:, 1] * h ** 2 / amax, c[:, 2] * h / amax, c[:, 3] / amax)
+        ext = []
+        for m in range(1, M - nint + 1):
+            ext.append(np.stack([d3, 3 * d3 * m + d2, (3 * d3 * m + 2 * d2) * m + d1,
+                                 ((d3 * m + d2) * m + d1) * m + d0], axis=-1))
+        tab = np.concatenate([np.asarray(tab, dtype=np.float32),
+                              np.stack(ext, axis=1).astype(np.float32)], axis=1)
+    return tab, M, M, None
 
 
 def _row_ids(portrait):

@@ -60,7 +60,12 @@ class Simulation(object):
     # -- stages (simulate.py:201-290) -----------------------------------------
     def init_signal(self, from_template=False):
         if from_template:
-            raise NotImplementedError("PSRFITS template signals are not on the device path")
+            # simulate.py:210-214 (note: the reference's simulate() never
+            # passes from_template=True through)
+            from ..io import PSRFITS
+            pfit = PSRFITS(path="sim_fits.fits", template=self.tempfile, fits_mode='copy', obs_mode='PSR')
+            self._signal = pfit.make_signal_from_psrfits()
+            return
         self._signal = FilterBankSignal(fcent=self.fcent, bandwidth=self.bw, Nsubband=self.Nchan,
                                         sample_rate=self.samprate, fold=self.fold, sublen=self.sublen,
                                         dtype=self.dtype, shard=self._shard)
@@ -129,16 +134,25 @@ class Simulation(object):
 
     def save_simulation(self, outfile="simfits", out_format='psrfits', parfile=None, ref_MJD=56000.0,
                         MJD_start=55999.9861):
-        """simulate.py:328-378.  'pdv' writes the PSRCHIVE pdv text format
-        (io.TxtFile); 'psrfits' needs the reference's template-copy writer
-        (pdat/fitsio/PINT polycos are not available) -> NotImplementedError
-        after the reference's own argument checks."""
+        """simulate.py:328-378.  'psrfits' copies the template file with the
+        reference's edits (io.PSRFITS; the POLYCO table stays the template's:
+        PINT is absent), 'pdv' writes the PSRCHIVE pdv text format
+        (io.TxtFile)."""
         if out_format.lower() == 'psrfits':
+            from ..io import PSRFITS
+            from ..utils import make_par
             if outfile == 'simfits':
                 outfile += ".fits"
             if self.tempfile is None:
                 raise RuntimeError("No template PSRFITS file provided.")
-            raise NotImplementedError("PSRFITS template output (pdat/fitsio/PINT) is not available")
+            pfit = PSRFITS(path=outfile, template=self.tempfile, fits_mode='copy', obs_mode='PSR')
+            pfit.get_signal_params(signal=self.signal)
+            if parfile is None:
+                log.warning("No par file provided, attempting to make one...")
+                make_par(self.signal, self.pulsar, outpar="simpar.par")
+                parfile = "simpar.par"
+            pfit.save(self.signal, self.pulsar, parfile=parfile, MJD_start=MJD_start, segLength=60.0,
+                      ref_MJD=ref_MJD, usePint=True)
         elif out_format.lower() == 'pdv':
             from ..io import TxtFile
             if outfile == 'simfits':

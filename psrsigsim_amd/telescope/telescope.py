@@ -135,6 +135,11 @@ class Telescope(object):
                                           _engine.stream_ptr())
             _lib.check(rc, "observe/clip")
         if ret_resampsig:
+            # the returned copy is a read-out of the data: a null() whose
+            # channel-0 maximum was not unique raises here, as the reference's
+            # null() would have (pulsar.py:286); without ret_resampsig the
+            # check stays deferred to the next read (no host sync per observe)
+            _engine.check_null_status(signal)
             return out
 
     def apply_response(self, signal):

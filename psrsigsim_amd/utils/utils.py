@@ -11,7 +11,7 @@ import torch
 from .._units import make_quant  # noqa: F401  (re-exported, utils.py:310)
 from .. import _engine, _lib
 
-__all__ = ["shift_t", "down_sample", "rebin", "make_quant", "top_hat_width"]
+__all__ = ["shift_t", "down_sample", "rebin", "make_quant", "top_hat_width", "make_par"]
 
 
 def _as_rows(y):
@@ -105,3 +105,31 @@ def top_hat_width(subband_df, subband_f0, DM):
     dispersion smearing 2 D DM df / f0^3 in ms, D = 4.148808e3 s MHz^2 cm^3/pc."""
     D = 4.148808e3
     return 2 * D * DM * subband_df / subband_f0 ** 3 * 1.0e+3
+
+
+# par-file lines of make_par after PSR / F0 / DM (utils.py:366-391)
+_PAR_DEFAULTS = [("LAMBDA", "            10.0"), ("BETA", "           10.0"), ("PMLAMBDA", "            0.0"),
+                 ("PMBETA", "            0.0"), ("PX", "            0.0"), ("POSEPOCH", "            56000.0")]
+_PAR_TAIL = [("PEPOCH", "            56000.0"), ("START", "            50000.0"), ("FINISH", "            60000.0")]
+_PAR_END = [("EPHEM", "               DE436"), ("SOLARN0", "               0.00"), ("ECL", "                 IERS2010"),
+            ("CLK", "                 TT(BIPM2015) "), ("UNITS", "               TDB"),
+            ("TIMEEPH", "             FB90"), ("T2CMETHOD", "           TEMPO"),
+            ("CORRECT_TROPOSPHERE", " N"), ("PLANET_SHAPIRO", "      N"), ("DILATEFREQ", "          N"),
+            ("TZRMJD", "        56000.0"), ("TZRFRQ", "            1500.0"), ("TZRSITE", "                  @"),
+            ("MODE", "                     1")]
+
+
+def make_par(signal, pulsar, outpar="simpar.par"):
+    """utils.py:350-395: a par file for the simulated pulsar (called by the
+    PSRFITS save path when no par file is given): PSR name, F0 = 1/period,
+    DM, and the reference's fixed defaults, one line each."""
+    period = float(getattr(pulsar.period, "value", pulsar.period))
+    dm = float(getattr(signal.dm, "value", signal.dm))
+    lines = ["PSR            %s\n" % (pulsar.name)]
+    lines += ["%s%s\n" % kv for kv in _PAR_DEFAULTS]
+    lines.append("F0           %s\n" % (1.0 / period))
+    lines += ["%s%s\n" % kv for kv in _PAR_TAIL]
+    lines.append("DM                %s\n" % (dm))
+    lines += ["%s%s\n" % kv for kv in _PAR_END]
+    with open(outpar, "w") as op:
+        op.writelines(lines)

@@ -48,13 +48,13 @@ def test_workspace_sizes():
     n = 1 << 20
     # pair mode: Yd ((nchan+2)//2 pairs, parity-aligned) + mask-table build (Mspec,
     # 6 node pair spills, 12 node rows, table bits/base, worst-case coefficients,
-    # misc) + per-channel null bits + row-pass ramp factors (64 complex per
-    # channel) + the null fix-up's word list (N/32 u32) + mask row -- no
+    # misc) + per-channel null bits + row-pass pair ramp factors (2 x 64
+    # complex per pair) + the null fix-up's word list (N/32 u32) + mask row -- no
     # per-channel mask spill
     table = n * 8 + 6 * n * 8 + 12 * n * 4 + (n // 32) * 8 + (n // 32) * 4 + n * 12 * 4 + 256
     wl = (n // 32) * 4
-    assert L.pss_workspace_bytes(4, n) == 3 * n * 8 + table + 4 * n // 8 + 4 * 512 + wl + n * 4
-    assert L.pss_workspace_bytes(3, n) == 2 * n * 8 + table + 3 * n // 8 + 3 * 512 + wl + n * 4
+    assert L.pss_workspace_bytes(4, n) == 3 * n * 8 + table + 4 * n // 8 + 3 * 1024 + wl + n * 4
+    assert L.pss_workspace_bytes(3, n) == 2 * n * 8 + table + 3 * n // 8 + 2 * 1024 + wl + n * 4
     sp = 2 * 2 * 244 * 8 + 244 * 8                                   # fallback W1, W2, twiddles
     assert L.pss_workspace_bytes(2, 244) == ((sp + 255) // 256) * 256 + 1024   # row: 976 B, aligned
     # Bluestein fallback (N > 8192, 2 x 5003): W1 only (forward and inverse

@@ -97,6 +97,27 @@ def test_odd_length_disperse_raises(hip_lib):
         ISM().disperse(sig, 10)
 
 
+def test_null_tied_channel0_raises_on_every_readout(hip_lib):
+    """A null() whose channel-0 maximum is not unique (the reference's
+    pulsar.py:286 broadcast ValueError) raises on observe's returned copy and on
+    every later read of the data, not only the first."""
+    import psrsigsim_amd as pss
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, DataProfile
+    from psrsigsim_amd.telescope import telescope as T
+    n = 1 << 14
+    sig = FilterBankSignal(1400, 400, Nsubband=2, fold=False)
+    psr = Pulsar(0.005, 1.0, profiles=DataProfile(np.ones(256), Nchan=2))
+    pss.inject(gen=np.ones((2, n)))            # flat channel 0: every sample ties
+    psr.make_pulses(sig, n * 20.48e-6)
+    psr.null(sig, 0.1)
+    with pytest.raises(ValueError):
+        T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True, ret_resampsig=True)
+    for _ in range(2):
+        with pytest.raises(ValueError):
+            sig.data
+
+
 def _big_case(log2n, nchan, null=True, fd=True):
     ops = [("scatter_conv", 1e-4, 1400, None), ("make_pulses", (1 << log2n) * 20.48e-6, "pulses"),
            ("disperse", 100, "disperse")]

@@ -188,7 +188,10 @@ def test_scatter_convolution_bitwise_vs_reference_structure(nchan):
     psr.make_pulses(sig, (1 << 16) * 20.48e-6)
     opsr.ref_freq = 1400.0
     O.add_spec_idx(osig, opsr)
-    assert sig._pending.source.nint == opsr.Profiles.knot_x.size - 1
+    # knot intervals (the periodic-closure decision); the device table itself
+    # always spans the period (nint == M, extrapolated pieces appended)
+    assert psr.Profiles.uniform_knots()[1] == opsr.Profiles.knot_x.size - 1
+    assert sig._pending.source.nint == sig._pending.source.M
 
 
 # ---------------------------------------------------------------------------

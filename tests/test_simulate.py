@@ -43,7 +43,7 @@ def test_init_stages_host():
     sim = _sim()
     sim.init_signal()
     assert sim.signal.Nchan == 64
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError):                  # no template file (tempfile=None)
         sim.init_signal(from_template=True)
     sim.init_profile()                               # None -> default Gaussian
     assert isinstance(sim.profiles, GaussPortrait)
