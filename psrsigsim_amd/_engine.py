@@ -69,6 +69,10 @@ def inject(**kw):
         _inject[k] = v
 
 
+class InjectedRowsMissing(KeyError):
+    """Injected draws (a RowBlock) that do not cover the requested channels."""
+
+
 class RowBlock(object):
     """Injected per-channel draws for global channels [c0, c0 + len(arr)) only
     (a shard's rows), instead of a full [Nchan, N] array."""
@@ -83,7 +87,7 @@ def inj_rows(inj, gidx):
     if isinstance(inj, RowBlock):
         rel = np.asarray(gidx) - inj.c0
         if rel.size and (rel.min() < 0 or rel.max() >= len(inj.arr)):
-            raise KeyError("injected rows cover channels [%d, %d), not %s"
+            raise InjectedRowsMissing("injected rows cover channels [%d, %d), not %s"
                            % (inj.c0, inj.c0 + len(inj.arr), list(np.asarray(gidx))))
         return np.asarray(inj.arr, dtype=np.float32)[rel]
     return np.asarray(inj, dtype=np.float32)[gidx]
@@ -345,7 +349,7 @@ def execute(sig, pend):
             sig._row0 = torch.empty((nrow, N), dtype=torch.float32, device=device())
         try:
             p0, k0 = build_pipeline(sig, pend, nrow, 0, sig._row0)
-        except KeyError:
+        except InjectedRowsMissing:
             # exact mode with draws injected for this shard's rows only: no
             # shadow (a later null() on this shard then needs the draws of
             # channels 0..1, and raises without them)

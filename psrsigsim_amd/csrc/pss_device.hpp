@@ -208,40 +208,82 @@ __device__ __forceinline__ float log1p_minus(float y) {
 }
 
 // chi2(df) for general df > 0 = 2 * Gamma(df/2) via Marsaglia-Tsang (2000);
-// shape < 1 boosted by U^(1/a).  The acceptance test ln u < z^2/2 + d(1 - v +
-// ln v), v = (1 + c z)^3, is evaluated in the cancellation-free form
-// d (3 (log1p(y) - y) - 3 y^2 - y^3), y = c z, so fp32 is exact enough even
-// at df ~ 1e4 (where d ~ 5e3 and the bracket is O(1/d)).
-// Each attempt consumes one Philox block keyed (a, b, attempt).
+// shape < 1 boosted by U^(1/a).  One attempt: z ~ N(0, 1), y = c z, v = (1 +
+// y)^3; accepted by the squeeze u < 1 - 0.0331 z^4 (no logarithm: ~all
+// attempts at the large df of fold mode, Nfold ~ 1e4) or else by ln u < z^2/2
+// + d (1 - v + ln v), evaluated in the cancellation-free form
+// d (3 (log1p(y) - y) - 3 y^2 - y^3) so fp32 is exact enough even at
+// df ~ 1e4 (d ~ 5e3, the bracket O(1/d)).
+struct MtParams {
+    float d, c, shape;
+    bool boost;
+};
+__device__ __forceinline__ MtParams mt_params(float df) {
+    MtParams q;
+    q.shape = 0.5f * df;
+    q.boost = q.shape < 1.0f;
+    q.d = (q.boost ? q.shape + 1.0f : q.shape) - (1.0f / 3.0f);
+    q.c = rsqrtf(9.0f * q.d);
+    return q;
+}
+__device__ __forceinline__ bool mt_try(float z, float u, const MtParams &q, float &x) {
+    const float y = q.c * z;
+    if (y <= -1.0f) return false;
+    const float v = (1.0f + y) * (1.0f + y) * (1.0f + y);
+    const float z2 = z * z;
+    if (u < fmaf(-0.0331f * z2, z2, 1.0f) ||
+        0.6931471805599453f * __builtin_amdgcn_logf(u) <
+            fmaf(0.5f, z2, q.d * (3.0f * log1p_minus(y) - y * y * (3.0f + y)))) {
+        x = q.d * v;
+        return true;
+    }
+    return false;
+}
+// Retries of sample h of a pair (rare): its own Philox block per attempt,
+// tags (h + 1) << 16 | t (attempt 0 is the pair's shared block, tag 1).
+__device__ __noinline__ float mt_retry(const Rng &g, uint32_t m, uint32_t b, uint32_t h, const MtParams &q) {
+    float x = q.d;
+    for (uint32_t t = 1; t < 64; ++t) {
+        const uint4 r = g.bits(m, b, ((h + 1u) << 16) | t);
+        const float z = sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01(r.x))) *
+                        __builtin_amdgcn_cosf(frac23(r.y));
+        if (mt_try(z, u01(r.z), q, x)) break;
+    }
+    return x;
+}
+// chi2(df) draws of the PAIR of samples (2m, 2m + 1) of stream position b:
+// attempt 0 of both comes from ONE Philox block -- the two Box-Muller normals
+// of (r.x, r.y), the uniforms r.z and r.w -- so a sample costs half a block,
+// half a logarithm and one sin or cos on the common path (fold-mode C4 draws
+// every sample this way).  Keyed (m, b, attempt): results do not depend on
+// how samples are grouped into launches.
+__device__ __forceinline__ void chi2_pair(const Rng &g, uint32_t m, uint32_t b, float df, float &x0, float &x1) {
+    const MtParams q = mt_params(df);
+    const uint4 r = g.bits(m, b, 1u);
+    const float sl = sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01(r.x)));
+    const float v = frac23(r.y);
+    const float z0 = sl * __builtin_amdgcn_cosf(v), z1 = sl * __builtin_amdgcn_sinf(v);
+    if (!mt_try(z0, u01(r.z), q, x0)) x0 = mt_retry(g, m, b, 0u, q);
+    if (!mt_try(z1, u01(r.w), q, x1)) x1 = mt_retry(g, m, b, 1u, q);
+    if (q.boost) {
+        const uint4 ub = g.bits(m, b, 0xFFFF0000u);
+        x0 *= __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(u01(ub.x)) / q.shape);
+        x1 *= __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(u01(ub.y)) / q.shape);
+    }
+    x0 *= 2.0f;
+    x1 *= 2.0f;
+}
+
+// One chi2(df) draw keyed (a, b): df == 1 -> the first z^2 of block (a, b, 0);
+// otherwise sample a of the pair sampler (pair a >> 1, half a & 1).
 __device__ __forceinline__ float chi2_general(const Rng &g, uint32_t a, uint32_t b, float df) {
     if (df == 1.0f) {
         float4 q = chi2_1x4(g.bits(a, b, 0));
         return q.x;
     }
-    const float shape = 0.5f * df;
-    const bool boost = shape < 1.0f;
-    const float aa = boost ? shape + 1.0f : shape;
-    const float d = aa - (1.0f / 3.0f);
-    const float c = rsqrtf(9.0f * d);
-    float x = d;
-    float ub = 0.5f;
-    for (uint32_t t = 0; t < 64; ++t) {
-        uint4 r = g.bits(a, b, t + 1);
-        const float l = -1.3862943611198906f * __builtin_amdgcn_logf(u01(r.x));
-        const float z = sqrtf(l) * __builtin_amdgcn_cosf(frac23(r.y));
-        const float y = c * z;
-        if (y <= -1.0f) continue;
-        const float lu = 0.6931471805599453f * __builtin_amdgcn_logf(u01(r.z));
-        const float rhs = 0.5f * z * z + d * (3.0f * log1p_minus(y) - y * y * (3.0f + y));
-        if (lu < rhs) {
-            const float v = (1.0f + y) * (1.0f + y) * (1.0f + y);
-            x = d * v;
-            ub = u01(r.w);
-            break;
-        }
-    }
-    if (boost) x *= __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(ub) / shape);
-    return 2.0f * x;
+    float x0, x1;
+    chi2_pair(g, a >> 1, b, df, x0, x1);
+    return (a & 1u) ? x1 : x0;
 }
 
 }  // namespace pss

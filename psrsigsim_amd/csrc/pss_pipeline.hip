@@ -235,6 +235,8 @@ __host__ __device__ __forceinline__ int64_t pstride(const KP &k) { return k.N1 *
 // nothing but a table lookup remains (no per-channel mask FFT or spill).
 // ---------------------------------------------------------------------------
 static constexpr int KCH = 12;
+// floats per f-dependent position record (root_hit): 16 (64 B, aligned)
+static constexpr int KREC = 16;
 // PCHIP intervals the fast pass A keeps in LDS (two rows; 69.7 KB FFT buffer +
 // 12 KB still allows two 512-thread workgroups per CU).
 static constexpr int kFastNint = 376;
@@ -263,14 +265,26 @@ __device__ __forceinline__ float cheb_eval_r(const float4 (&q)[3], float t) {
 }
 
 // Decision of an f-dependent position from its ROOT record (k_mask_table):
-// rec = {count, s0, r_1 .. r_10}: the fp32 Chebyshev value at t exceeds 1
+// rec = {count, s0, r_1 .. r_10, -}: the fp32 Chebyshev value at t exceeds 1
 // iff s0 XOR (the number of roots r_i < t) is odd.  The roots are where
-// cheb_eval_r(c, .) > 1 flips (33-point scan of t in [-1, 1], 24 bisection
-// steps each), so the rule reproduces the direct evaluation except within
-// ~1e-8 of a flip, with one 16-B load and two compares per position instead
-// of 48 B of coefficients and a 12-term Clenshaw sum; unused roots are +inf.
-// `a` is the record's first float4.
+// cheb_eval_r(c, .) > 1 flips, found by a 129-point scan of t in [-1, 1]
+// (24 bisection steps per flip) whose cells are CERTIFIED to hold no hidden
+// pair of flips: a cell without a sign change holds no root when |g(t_j)| +
+// |g(t_j+1)| > h max|g'|, and one with a sign change holds exactly one when
+// the secant |g(t_j+1) - g(t_j)| / h exceeds h max|g''| (g = value - 1, the
+// Markov bounds max|T_n'| = n^2, max|T_n''| = n^2 (n^2 - 1) / 3, fp32
+// evaluation error included).  The rule then reproduces the direct
+// evaluation except within ~1e-8 of a flip, with one 16-B load and two
+// compares per position instead of 48 B of coefficients and a 12-term
+// Clenshaw sum; unused roots are +inf.  A position whose cells cannot all be
+// certified keeps its coefficients instead: rec = {-1, -, -, -, c_0 .. c_11},
+// evaluated directly.  `a` is the record's first float4.
 __device__ __forceinline__ bool root_hit(const float4 a, const float *rec, float t) {
+    if (a.x < 0.f) {                     // uncertified: the coefficient record
+        const float4 q[3] = {reinterpret_cast<const float4 *>(rec)[1], reinterpret_cast<const float4 *>(rec)[2],
+                             reinterpret_cast<const float4 *>(rec)[3]};
+        return cheb_eval_r(q, t) > 1.0f;
+    }
     bool h = (a.y != 0.f) ^ (t > a.z) ^ (t > a.w);
     if (a.x > 2.f) {                    // rare: more than two flips over f in [0, 1)
         const float4 b = reinterpret_cast<const float4 *>(rec)[1], c = reinterpret_cast<const float4 *>(rec)[2];
@@ -297,7 +311,7 @@ __device__ __forceinline__ uint32_t mask_hits4(const KP &k, int64_t n0, uint32_t
                 const uint32_t p = (p0 + (uint32_t)i) & nm, pw = p >> 5;
                 const uint32_t word = (pw == w) ? A.y : Bw.y;
                 const uint32_t idx = k.mt_base[pw] + (uint32_t)__popc(word & ((1u << (p & 31u)) - 1u));
-                const float *rec = k.mt_coef + (int64_t)idx * KCH;
+                const float *rec = k.mt_coef + (int64_t)idx * KREC;
                 const bool hit = root_hit(reinterpret_cast<const float4 *>(rec)[0], rec, t);
                 r = (r & ~(1u << i)) | ((uint32_t)hit << i);
             }
@@ -337,7 +351,7 @@ __device__ __forceinline__ uint32_t mask_run(const KP &k, uint32_t n, uint32_t i
         const float *rec[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            rec[u] = k.mt_coef + (int64_t)(ii[u] < 32u ? idx[u] : idx[0]) * KCH;
+            rec[u] = k.mt_coef + (int64_t)(ii[u] < 32u ? idx[u] : idx[0]) * KREC;
             a[u] = reinterpret_cast<const float4 *>(rec[u])[0];
         }
 #pragma unroll
@@ -590,14 +604,16 @@ __device__ __forceinline__ float box_value(const KP &k, int64_t n, int rank, int
 }
 
 // chi2 draws for 4 consecutive samples n0..n0+3 (n0 % 4 == 0) of channel c.
-// df == 1: one Philox block per 4 samples; otherwise Marsaglia-Tsang per sample.
+// df == 1: one Philox block per 4 samples; otherwise the Marsaglia-Tsang
+// pair sampler, one shared block per 2 samples (chi2_pair).
 __device__ __forceinline__ void draw4(const Rng &g, int64_t n0, uint32_t c, float df, float (&x)[4]) {
     if (df == 1.0f) {
         float4 q = chi2_1x4(g.bits((uint32_t)(n0 >> 2), c, (uint32_t)(n0 >> 34)));
         x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
     } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) x[i] = chi2_general(g, (uint32_t)(n0 + i), c, df);
+        const uint32_t m = (uint32_t)(n0 >> 1);
+        chi2_pair(g, m, c, df, x[0], x[1]);
+        chi2_pair(g, m + 1u, c, df, x[2], x[3]);
     }
 }
 
@@ -1955,20 +1971,35 @@ __global__ __launch_bounds__(256) void k_mask_table(const float *nodes, int64_t 
         base[(p >> 5) + 1] = b0 + (uint32_t)__popc((uint32_t)ab);
     }
     if (amb) {
-        // root record (root_hit): where the fp32 Clenshaw value crosses 1
+        // root record (root_hit): where the fp32 Clenshaw value crosses 1,
+        // on a certified scan grid (see root_hit)
         const float4 q[3] = {make_float4(c[0], c[1], c[2], c[3]), make_float4(c[4], c[5], c[6], c[7]),
                              make_float4(c[8], c[9], c[10], c[11])};
+        float D1 = 0.f, D2 = 0.f;                    // max |g'|, max |g''| on [-1, 1]
+#pragma unroll
+        for (int n = 1; n < KCH; ++n) {
+            const float a = fabsf(c[n]), n2 = (float)(n * n);
+            D1 = fmaf(n2, a, D1);
+            D2 = fmaf(n2 * (n2 - 1.0f) * (1.0f / 3.0f), a, D2);
+        }
+        const float err = 4e-6f * (fabsf(c[0]) + S);  // fp32 Clenshaw error bound (as eps)
+        constexpr int NG = 128;
+        constexpr float H = 2.0f / NG;
         float rt[10];
 #pragma unroll
         for (int i = 0; i < 10; ++i) rt[i] = INFINITY;
-        bool prev = cheb_eval_r(q, -1.0f) > 1.0f;
+        float gprev = cheb_eval_r(q, -1.0f) - 1.0f;
+        bool prev = gprev > 0.0f;
         const bool s0 = prev;
+        bool cert = true;
         int cnt = 0;
         float tprev = -1.0f;
-        for (int jg = 1; jg <= 32; ++jg) {
-            const float tg = -1.0f + (float)jg * 0.0625f;
-            const bool cur = cheb_eval_r(q, tg) > 1.0f;
+        for (int jg = 1; jg <= NG; ++jg) {
+            const float tg = -1.0f + (float)jg * H;
+            const float g = cheb_eval_r(q, tg) - 1.0f;
+            const bool cur = g > 0.0f;
             if (cur != prev) {
+                cert = cert && (fabsf(g - gprev) - 2.0f * err > D2 * H * H);   // one flip only
                 float lo = tprev, hi = tg;            // decision prev at lo, cur at hi
                 for (int it = 0; it < 24; ++it) {
                     const float mid = 0.5f * (lo + hi);
@@ -1977,15 +2008,25 @@ __global__ __launch_bounds__(256) void k_mask_table(const float *nodes, int64_t 
 #pragma unroll
                 for (int i = 0; i < 10; ++i) if (i == cnt) rt[i] = lo;
                 ++cnt;
+            } else {
+                cert = cert && (fabsf(g) + fabsf(gprev) - 2.0f * err > D1 * H);   // no flip
             }
             prev = cur;
+            gprev = g;
             tprev = tg;
         }
         const uint32_t idx = b0 + (uint32_t)__popcll(ab & ((1ull << lane) - 1ull));
-        float4 *dst = reinterpret_cast<float4 *>(coef + (int64_t)idx * KCH);
-        dst[0] = make_float4((float)min(cnt, 10), s0 ? 1.0f : 0.0f, rt[0], rt[1]);
-        dst[1] = make_float4(rt[2], rt[3], rt[4], rt[5]);
-        dst[2] = make_float4(rt[6], rt[7], rt[8], rt[9]);
+        float4 *dst = reinterpret_cast<float4 *>(coef + (int64_t)idx * KREC);
+        if (cert && cnt <= 10) {
+            dst[0] = make_float4((float)cnt, s0 ? 1.0f : 0.0f, rt[0], rt[1]);
+            dst[1] = make_float4(rt[2], rt[3], rt[4], rt[5]);
+            dst[2] = make_float4(rt[6], rt[7], rt[8], rt[9]);
+        } else {
+            dst[0] = make_float4(-1.0f, 0.0f, 0.0f, 0.0f);
+            dst[1] = q[0];
+            dst[2] = q[1];
+            dst[3] = q[2];
+        }
     }
 }
 
@@ -2483,7 +2524,7 @@ using C8kI = RList<8, 8, 8, 16>;
 //   four-step (N = 2^m, 2^14 <= N <= 2^24):
 //     Yd [npairs][N] cf | Mspec [N] cf | node spill [KCH/2][N] cf |
 //     nodes [KCH][N] f32 | table bits [N/64] uint4 | base [N/64] u32 |
-//     coef [N][KCH] f32 (worst case) | misc (counter, node ramps/nyq) |
+//     coef [N][KREC] f32 (worst case) | misc (counter, node ramps/nyq) |
 //     null bits [nchan][N/32] u32 | mask row [N] f32
 //   single pass (N <= 8192): mask row
 //   direct DFT fallback: W1, W2 [nchan][N] cf | twiddles [N] cf | mask row
@@ -2552,7 +2593,7 @@ static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
         w.nodes = o; o += al256((int64_t)KCH * N * 4);
         w.bits = o;  o += al256((N / 32) * 8);
         w.base = o;  o += al256((N / 32) * 4);
-        w.coef = o;  o += al256(N * KCH * 4);
+        w.coef = o;  o += al256(N * KREC * 4);
         w.misc = o;  o += 256;
         w.mbits = o; o += al256((int64_t)nchan * (N / 8));   // per-channel null bits
         w.rtab = o;  o += al256(npairs * 2 * 64 * 8);          // row-pass pair ramp factors (RFL <= 64)

@@ -86,6 +86,13 @@ class RowSet(object):
 
     def __init__(self, c0, c1, nglobal, group):
         import numpy as np
+        # the reductions run on CPU tensors: the group needs a host backend
+        # (an NCCL/RCCL group would fail or hang here; bench.py makes a gloo
+        # group next to the RCCL one)
+        backend = str(dist.get_backend(group)).lower()
+        if backend not in ("gloo", "mpi"):
+            raise ValueError("plan_group must be a CPU (gloo) process group, got backend %r: create one with "
+                             "torch.distributed.new_group(backend='gloo')" % backend)
         self.c0, self.c1, self.nglobal, self.group = int(c0), int(c1), int(nglobal), group
         head = [c for c in (0, 1) if c < self.nglobal and not c0 <= c < c1]
         self.gids = np.array(sorted(set(head) | set(range(self.c0, self.c1))), dtype=np.int64)

@@ -156,6 +156,20 @@ def oracle_exec(case, d):
             O.scatter_broaden(sig, op[1], op[2], convolve=False)
         elif k == "scatter_conv":
             O.scatter_broaden(sig, op[1], op[2], convolve=True, pulsar=psr)
+        elif k == "scatter_tail":
+            # EXTENSION (no reference counterpart): the
+            # float64 restatement of scatter_broaden(tail=True) -- every row
+            # circularly convolved with (1 - a) a^n, a = exp(-dt / tau_c),
+            # tau_c = tau_d (f_c / f_ref)^(-22/5); a filter, not a delay, so
+            # signal.delay (and the null mask) are untouched
+            x = np.asarray(sig.data, dtype=np.float64)
+            n = x.shape[1]
+            f = np.asarray(sig.dat_freq, dtype=np.float64)
+            tau_ms = op[1] * 1e3 * (f / op[2]) ** (-22.0 / 5.0)
+            a = np.exp(-(1e-3 / sig.samprate) / tau_ms)[:, None]          # dt in ms (samprate in MHz)
+            kk = np.arange(n // 2 + 1)[None, :]
+            H = (1 - a) / (1 - a * np.exp(-2j * np.pi * kk / n))
+            sig.data = np.fft.irfft(np.fft.rfft(x, axis=1) * H, n=n, axis=1)
         elif k == "null":
             pre_max = np.max(np.abs(np.asarray(sig.data, dtype=np.float64)), axis=1)
             info = O.null(sig, psr, op[1], d)
@@ -306,6 +320,9 @@ def run_case(name, fused=True, case=None, seed=None):
             snap(op[3])
         elif k == "scatter_conv":
             ism.scatter_broaden(sig, op[1], op[2], convolve=True, pulsar=psr)
+        elif k == "scatter_tail":
+            ism.scatter_broaden(sig, op[1], op[2], tail=True)
+            snap(op[3])
         elif k == "null":
             pss.inject(null_pulses=inj["null_pulses"], box=inj["box"])
             if inj["rep"] is not None:

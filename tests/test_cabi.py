@@ -47,11 +47,11 @@ def test_workspace_sizes():
     assert L.pss_workspace_bytes(4, 4096) == 4096 * 4               # single pass: LDS only
     n = 1 << 20
     # pair mode: Yd ((nchan+2)//2 pairs, parity-aligned) + mask-table build (Mspec,
-    # 6 node pair spills, 12 node rows, table bits/base, worst-case coefficients,
+    # 6 node pair spills, 12 node rows, table bits/base, worst-case 16-float records,
     # misc) + per-channel null bits + row-pass pair ramp factors (2 x 64
     # complex per pair) + the null fix-up's word list (N/32 u32) + mask row -- no
     # per-channel mask spill
-    table = n * 8 + 6 * n * 8 + 12 * n * 4 + (n // 32) * 8 + (n // 32) * 4 + n * 12 * 4 + 256
+    table = n * 8 + 6 * n * 8 + 12 * n * 4 + (n // 32) * 8 + (n // 32) * 4 + n * 16 * 4 + 256
     wl = (n // 32) * 4
     assert L.pss_workspace_bytes(4, n) == 3 * n * 8 + table + 4 * n // 8 + 3 * 1024 + wl + n * 4
     assert L.pss_workspace_bytes(3, n) == 2 * n * 8 + table + 3 * n // 8 + 2 * 1024 + wl + n * 4

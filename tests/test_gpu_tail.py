@@ -101,3 +101,22 @@ def test_tail_with_delayed_null_off_fourstep_is_unsupported(hip_lib):
     psr.null(sig, 0.3)
     with pytest.raises(NotImplementedError):
         _ = sig.data
+
+
+def test_tail_disperse_delayed_null_2p22_vs_oracle(hip_lib):
+    """The tail extension together with disperse and a DELAYED null at the
+    north-star length 2^22 on the pair four-step (the mask-table null path):
+    against the oracle run with injected draws (legacy RandomState) and the
+    float64 restatement of the tail (tests/replay.py 'scatter_tail'; the tail
+    is a filter, so the null mask is shifted by the dispersion delay only,
+    pulsar.py:306-330)."""
+    from tests import replay
+    case = dict(sig=dict(fcent=1400, bw=400, nchan=2, fold=False),
+                psr=dict(period=0.005, Smean=1.0, prof=("gauss", 0.5, 0.05, 1)),
+                ops=[("make_pulses", (1 << 22) * 20.48e-6, "pulses"), ("scatter_tail", 2e-4, 1400.0, None),
+                     ("disperse", 100, "disperse"), ("null", 0.1, "null"),
+                     ("observe", "Arecibo", "Lband_PUPPI", True, "noise")])
+    errs = replay.run_case(None, fused=True, case=case, seed=2222)
+    bad = {k: v for k, v in errs.items() if not v <= TOL}
+    assert errs and not bad, errs
+    assert replay.STATS.get("ambiguous_path") == "table"

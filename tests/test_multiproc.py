@@ -207,3 +207,12 @@ def test_bench_self_launch_world2():
         assert line["config"]["nchan_total"] == (16 if scaling == "weak" else 8)
         assert line["config"]["nchan_per_gpu"] == (8 if scaling == "weak" else 4)
         assert line["value"] > 0
+
+
+def test_rowset_requires_host_backend(monkeypatch):
+    """shard.RowSet reduces CPU tensors: an NCCL/RCCL plan_group is refused
+    with a clear error instead of failing or hanging inside a collective."""
+    from psrsigsim_amd import shard
+    monkeypatch.setattr(shard.dist, "get_backend", lambda group=None: "nccl")
+    with pytest.raises(ValueError, match="gloo"):
+        shard.RowSet(0, 4, 4, object())

@@ -25,6 +25,13 @@ if [ -n "$OLD" ]; then
   done
   unset PSS_LIB_PATH
 fi
+# strong-scaling per-rank share of C3 on one GPU: 256 ch (N = 8), 512 ch (N = 4)
+for nc in 256 512; do
+  timeout -k 10 300 python bench.py --no-cpu --steps 30 --nchan $nc > $OUT/bench_${TAG}_n$nc.json 2> $OUT/bench_${TAG}_n$nc.err \
+    || { echo "nchan $nc failed"; tail -3 $OUT/bench_${TAG}_n$nc.err; exit 1; }
+  python -c "import json; d=json.load(open('$OUT/bench_${TAG}_n$nc.json')); print('nchan', $nc, d['ms_per_step'], 'steady', d['step_ms_steady'], 'first', d['step_ms_first'], 'kern', round(d['gpu_kernel_ms_per_step'],3))"
+done
+timeout -k 10 300 python tools/step_timeline.py 256 > $OUT/timeline_${TAG}_256.log 2>&1 || exit $?
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- \
     python $R/bench.py --steps 3 --warmup 1 --no-cpu > $OUT/prof_$TAG.log 2>&1 || exit $?
