@@ -61,12 +61,13 @@ TOBS_PER_SAMPLE = 20.48e-6
 # value (pair mode), i.e. 4 B per channel-sample per spill pass; the null mask
 # is a once-per-run table (no per-channel bytes).
 #   colA: write spill 4 | row: read 4 + write 4 | colC: read spill 4 + write fp32 4
-#   null_fix: rewrite the nulled samples, 4 B each: C3's null(0.1) nulls
-#   round(0.1 nsub) whole periods of Nph samples, ~0.1 of every channel
-#   (PMC, profiles/r02: 5.57 GB of writes per launch = 0.65 B/ch-sample; the
-#   kernel writes whole 16-B groups, and the shifted boxes' ringing crosses the
-#   threshold around the nulled periods too)
-NULL_FRAC_C3 = 0.1
+#   null_fix: rewrite the nulled samples, 4 B each.  C3's null(0.1) picks
+#   round(0.1 nsub) whole periods, but the reference thresholds the FFT-shifted
+#   chi2(100) box mask at > 1 (pulsar.py:306-330), and the boxes' Gibbs ringing
+#   crosses that threshold around every nulled period too: ~16 % of each
+#   channel's samples end up nulled (PMC, profiles/r02: 5.57 GB of writes per
+#   launch = 0.65 B/ch-sample), so that measured fraction is what is booked
+NULL_FRAC_C3 = 0.16
 ALG_BYTES = {"fourstep_colA": 4.0, "fourstep_row": 8.0, "fourstep_colC": 8.0, "null_fix": 4.0 * NULL_FRAC_C3,
              "single_pass": 4.0, "elementwise": 8.0, "fallback_dft": 28.0}
 
@@ -557,12 +558,14 @@ def main():
                 "avg_launch_ms": round(avg_ms, 4), "alg_bytes_per_launch": bytes_launch}
         # measured HBM bytes per launch of this kernel (rocprofv3 PMC passes,
         # tools/pmc_round.sh + tools/pmc_traffic.py; C3 size only)
-        tj = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
-        if args.workload == "c3" and C == NCHAN and nsamp == (1 << LOG2N) and os.path.exists(tj):
-            t = json.load(open(tj)).get(dom)
-            if t:
-                roof["traffic"] = round(t["traffic_bytes"] / 1e9, 3)
-                roof["traffic_unit"] = "GB per launch (PMC, profiles/r02/pmc_traffic.json)"
+        for rnd in ("r03", "r02"):
+            tj = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
+            if args.workload == "c3" and C == NCHAN and nsamp == (1 << LOG2N) and os.path.exists(tj):
+                t = json.load(open(tj)).get(dom)
+                if t:
+                    roof["traffic"] = round(t["traffic_bytes"] / 1e9, 3)
+                    roof["traffic_unit"] = "GB per launch (PMC, profiles/%s/pmc_traffic.json)" % rnd
+                break                           # the newest round's passes only
 
     cpu = None
     cpu_all = None

@@ -151,6 +151,34 @@ struct Lds {
 template <int... Rs>
 struct RList {};
 
+// LDS byte addressing.  With the swizzled layout, a row pitch RS that is a
+// multiple of 16 complex and an LDS buffer aligned to 128 B, the positions a
+// Stockham scatter writes -- base + q (Ns = 1) or base + 16 q (Ns = 16) -- sit
+// at byte address (A ^ 8q) (+ 128 q): the swizzle XOR of the position's low
+// four bits with q folds into ONE v_xor per value on a per-thread byte base
+// (the index form costs an XOR and a shift-add per value), and gathers with a
+// stride that is a multiple of 256 positions are a base plus immediate
+// offsets.  Fft<..., XRS> selects it when Lds<L, XRS>::RS % 16 == 0
+// (PSS_LDS_XB); the caller then owes the 128-B alignment of the buffer.
+#ifndef PSS_LDS_XB
+#define PSS_LDS_XB 1
+#endif
+typedef float lds_f2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) lds_f2 lds_f2_t;
+__device__ __forceinline__ uint32_t lds_byte(const cf *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+__device__ __forceinline__ void lds_st(uint32_t a, cf v) {
+    lds_f2 w;
+    w.x = v.x;
+    w.y = v.y;
+    *(lds_f2_t *)(uintptr_t)a = w;
+}
+__device__ __forceinline__ cf lds_ld(uint32_t a) {
+    const lds_f2 w = *(const lds_f2_t *)(uintptr_t)a;
+    return make_float2(w.x, w.y);
+}
+
 // Synchronisation between the Stockham stages' LDS exchanges.  WAVE = true:
 // the transform belongs to ONE wave (T = 64 lanes, its own LDS region), so
 // the exchange only needs the wave's own LDS operations ordered -- no
@@ -253,6 +281,8 @@ __device__ __forceinline__ void tw16_fill(cf *tw16, int tid, int nthreads) {
 template <int L, int BATCH, int T, bool WAVE = false, int XRS = 1>
 struct Fft {
     using LD = Lds<L, XRS>;
+    // byte-address forms of the exchanges (see lds_byte)
+    static constexpr bool XB = PSS_LDS_XB && LD::SWZ && (LD::RS % 16 == 0);
     static constexpr int E = L * BATCH / T;
     static_assert(E * T == L * BATCH, "T must divide L*BATCH");
     static_assert(!WAVE || (T == 64 && BATCH == 1), "a wave-local transform is one sequence on 64 lanes");
@@ -264,8 +294,15 @@ struct Fft {
 #pragma unroll
         for (int ib = 0; ib < E / R0; ++ib) {
             const int j = tid + ib * T, b = j / LR, jj = j - b * LR;
+            if constexpr (XB && LR % 256 == 0) {
+                // positions jj + q LR: the swizzle XOR (jj >> 4) & 15 is the same for every q
+                const uint32_t a = lds_byte(lds) + 8u * (uint32_t)LD::at(b, jj);
 #pragma unroll
-            for (int q = 0; q < R0; ++q) v[ib * R0 + q] = lds[LD::at(b, jj + q * LR)];
+                for (int q = 0; q < R0; ++q) v[ib * R0 + q] = lds_ld(a + 8u * (uint32_t)(q * LR));
+            } else {
+#pragma unroll
+                for (int q = 0; q < R0; ++q) v[ib * R0 + q] = lds[LD::at(b, jj + q * LR)];
+            }
         }
     }
     // Store registers (last-stage OUTPUT mapping of radix R) to LDS, natural.
@@ -364,8 +401,28 @@ struct Fft {
                 const int j = tid + ib * T, b = j / LR, jj = j - b * LR;
                 const int k = jj % Ns;
                 const int base = (jj / Ns) * Ns * R + k;
+                if constexpr (XB && 16 % R == 0 && Ns == 1) {
+                    // positions base + q, base = R jj: at = X ^ q
+                    const uint32_t a = lds_byte(lds) + 8u * (uint32_t)(b * LD::RS + (base ^ ((base >> 4) & 15)));
 #pragma unroll
-                for (int q = 0; q < R; ++q) lds[LD::at(b, base + q * Ns)] = v[ib * R + q];
+                    for (int q = 0; q < R; ++q) lds_st(a ^ (8u * (uint32_t)q), v[ib * R + q]);
+                } else if constexpr (XB && 16 % R == 0 && Ns == 16) {
+                    // positions base + 16 q, base = 16 R G + k (G = jj / 16):
+                    // the swizzle XOR is c | q, c = (R G) & 15, so at = (X ^ q) + 16 q
+                    // with X = b RS + (base ^ c)
+                    const int c = ((jj / Ns) * R) & 15;
+                    const uint32_t a = lds_byte(lds) + 8u * (uint32_t)(b * LD::RS + (base ^ c));
+#pragma unroll
+                    for (int q = 0; q < R; ++q) lds_st((a ^ (8u * (uint32_t)q)) + 128u * (uint32_t)q, v[ib * R + q]);
+                } else if constexpr (XB && Ns % 256 == 0) {
+                    // positions base + Ns q: the swizzle XOR is the same for every q
+                    const uint32_t a = lds_byte(lds) + 8u * (uint32_t)LD::at(b, base);
+#pragma unroll
+                    for (int q = 0; q < R; ++q) lds_st(a + 8u * (uint32_t)(q * Ns), v[ib * R + q]);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < R; ++q) lds[LD::at(b, base + q * Ns)] = v[ib * R + q];
+                }
             }
             stage_sync<WAVE>();
             constexpr int R2 = first<Rest...>();

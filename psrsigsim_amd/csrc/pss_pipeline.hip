@@ -267,13 +267,15 @@ __device__ __forceinline__ float cheb_eval_r(const float4 (&q)[3], float t) {
 // Decision of an f-dependent position from its ROOT record (k_mask_table):
 // rec = {count, s0, r_1 .. r_10, -}: the fp32 Chebyshev value at t exceeds 1
 // iff s0 XOR (the number of roots r_i < t) is odd.  The roots are where
-// cheb_eval_r(c, .) > 1 flips, found by a 129-point scan of t in [-1, 1]
+// cheb_eval_r(c, .) > 1 flips, found by a 257-point scan of t in [-1, 1]
 // (24 bisection steps per flip) whose cells are CERTIFIED to hold no hidden
-// pair of flips: a cell without a sign change holds no root when |g(t_j)| +
-// |g(t_j+1)| > h max|g'|, and one with a sign change holds exactly one when
-// the secant |g(t_j+1) - g(t_j)| / h exceeds h max|g''| (g = value - 1, the
-// Markov bounds max|T_n'| = n^2, max|T_n''| = n^2 (n^2 - 1) / 3, fp32
-// evaluation error included).  The rule then reproduces the direct
+// pair of flips (g = value - 1, D2 = max|g''| <= sum_n |c_n| n^2 (n^2 - 1) / 3
+// by Markov's bound on T_n'', fp32 evaluation error included): a cell whose
+// ends share a sign holds no root when min(|g(t_j)|, |g(t_j+1)|) > D2 h^2 / 8
+// (the chord-interpolation error bound), and one with a sign change holds
+// exactly one when the secant |g(t_j+1) - g(t_j)| / h exceeds D2 h (g' keeps
+// its sign; ~2 % of the f-dependent positions of C3's mask fail this and keep
+// coefficient records, measured with tools/mask_cert.py).  The rule then reproduces the direct
 // evaluation except within ~1e-8 of a flip, with one 16-B load and two
 // compares per position instead of 48 B of coefficients and a 12-term
 // Clenshaw sum; unused roots are +inf.  A position whose cells cannot all be
@@ -1242,7 +1244,11 @@ struct PairRows;
 
 template <int N2, int T, int... F, int... I>
 struct PairRows<N2, T, RList<F...>, RList<I...>> {
-    using FF = Fft<N2, 2, T>;
+    // row pitch N2 + 16 (a multiple of 16 complex: the byte-address XOR
+    // exchanges, Fft::XB; the rows' bank offset is irrelevant here -- every
+    // wave works on one row per instruction)
+    using FF = Fft<N2, 2, T, false, 16>;
+    using LD = typename FF::LD;
     static constexpr int E = FF::E;
     static constexpr int RF0 = FF::template first<F...>();
     static constexpr int RFL = FF::template last_of<F...>();
@@ -1263,7 +1269,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
     //               once-per-run mask spectrum times each node's ramp.
     template <bool MASK, bool TAIL = false>
     __device__ static void pass(const KP &k) {
-        __shared__ cf lds[2 * Lds<N2>::RS];
+        __shared__ __align__(128) cf lds[2 * LD::RS];
         __shared__ cf tw16[kTw16Size];
         const int tid = threadIdx.x;
         tw16_fill(tw16, tid, T);     // first read after the first stage's barrier
@@ -1304,13 +1310,27 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                 const int64_t kb0 = row + (int64_t)N1 * jj;
                 const cf bE = expi_rev(-fix_to_rev((uint64_t)kb0 * hsum));
                 const cf bD = expi_rev(-fix_to_rev((uint64_t)kb0 * hdif));
+                // mirror bins k2m = N2 - 1 - k2 = P0 - q LRL (all but row 0 of
+                // the {0, N1/2} pair, whose bin 0 pairs with itself): with
+                // LRL % 256 == 0 the swizzle XOR is the same for every q, so
+                // the reads are one byte base minus immediate offsets
+                constexpr bool kMirXB = FF::XB && (LRL % 256 == 0);
+                const bool affine = !(j == 0 && row == 0);       // wave-uniform
+                uint32_t mbase = 0;
+                if constexpr (kMirXB) mbase = lds_byte(lds) + 8u * (uint32_t)LD::at(j == 0 ? b : 1 - b, N2 - 1 - jj);
 #pragma unroll
                 for (int q = 0; q < RFL; ++q) {
                     const int i = ib * RFL + q, k2 = jj + q * LRL;
-                    int bm, k2m;
-                    if (j == 0) { bm = b; k2m = (row == 0) ? ((N2 - k2) & (N2 - 1)) : (N2 - 1 - k2); }
-                    else        { bm = 1 - b; k2m = N2 - 1 - k2; }
-                    const cf Z = v[i], Zm = lds[Lds<N2>::at(bm, k2m)];
+                    cf Zm;
+                    if (kMirXB && affine) {
+                        Zm = lds_ld(mbase - 8u * (uint32_t)(q * LRL));
+                    } else {
+                        int bm, k2m;
+                        if (j == 0) { bm = b; k2m = (row == 0) ? ((N2 - k2) & (N2 - 1)) : (N2 - 1 - k2); }
+                        else        { bm = 1 - b; k2m = N2 - 1 - k2; }
+                        Zm = lds[LD::at(bm, k2m)];
+                    }
+                    const cf Z = v[i];
                     // 2 D_a and 2 D_b (DC / Nyquist and the tail extension)
                     const cf Sa = make_float2(Z.x + Zm.x, Z.y - Zm.y);
                     const cf Sb = make_float2(Z.y + Zm.y, Zm.x - Z.x);
@@ -1975,15 +1995,14 @@ __global__ __launch_bounds__(256) void k_mask_table(const float *nodes, int64_t 
         // on a certified scan grid (see root_hit)
         const float4 q[3] = {make_float4(c[0], c[1], c[2], c[3]), make_float4(c[4], c[5], c[6], c[7]),
                              make_float4(c[8], c[9], c[10], c[11])};
-        float D1 = 0.f, D2 = 0.f;                    // max |g'|, max |g''| on [-1, 1]
+        float D2 = 0.f;                              // max |g''| on [-1, 1] (Markov)
 #pragma unroll
-        for (int n = 1; n < KCH; ++n) {
-            const float a = fabsf(c[n]), n2 = (float)(n * n);
-            D1 = fmaf(n2, a, D1);
-            D2 = fmaf(n2 * (n2 - 1.0f) * (1.0f / 3.0f), a, D2);
+        for (int n = 2; n < KCH; ++n) {
+            const float n2 = (float)(n * n);
+            D2 = fmaf(n2 * (n2 - 1.0f) * (1.0f / 3.0f), fabsf(c[n]), D2);
         }
         const float err = 4e-6f * (fabsf(c[0]) + S);  // fp32 Clenshaw error bound (as eps)
-        constexpr int NG = 128;
+        constexpr int NG = 256;
         constexpr float H = 2.0f / NG;
         float rt[10];
 #pragma unroll
@@ -2009,7 +2028,9 @@ __global__ __launch_bounds__(256) void k_mask_table(const float *nodes, int64_t 
                 for (int i = 0; i < 10; ++i) if (i == cnt) rt[i] = lo;
                 ++cnt;
             } else {
-                cert = cert && (fabsf(g) + fabsf(gprev) - 2.0f * err > D1 * H);   // no flip
+                // no flip: g stays within D2 H^2 / 8 of the chord between the
+                // cell's ends, whose values share a sign
+                cert = cert && (fminf(fabsf(g), fabsf(gprev)) - err > D2 * H * H * 0.125f);
             }
             prev = cur;
             gprev = g;

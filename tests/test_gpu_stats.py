@@ -22,11 +22,19 @@ def _fill(df, rows=2, n=1 << 20, purpose=5, call=7):
 
 @pytest.mark.parametrize("df", [1.0, 0.5, 3.7, 100.0, 11190.0])
 def test_chi2_draws_distribution(df, hip_lib):
-    x = _fill(df)
+    """Mean within 0.5 % and variance within 1 % of chi2(df) per row (or 4
+    standard errors, whichever is larger: chi2's fourth central moment is
+    12 df (df + 4), so at df = 0.5 the sample variance of 2^20 draws has a
+    0.5 % standard error -- 2^24 draws per row are used for df < 2), plus a
+    KS test (p > 0.01)."""
+    n = 1 << (24 if df < 2 else 20)
+    x = _fill(df, n=n)
+    se_m = np.sqrt(2.0 / (df * n))                                   # relative SE of the mean
+    se_v = np.sqrt((12.0 * df * (df + 4) - 4.0 * df * df) / n) / (2.0 * df)   # ... of the variance
     for row in x:
         m, v = row.mean(), row.var()
-        assert abs(m / df - 1) < 5e-3, (df, m)
-        assert abs(v / (2 * df) - 1) < 1e-2, (df, v)
+        assert abs(m / df - 1) < max(5e-3, 4 * se_m), (df, m)
+        assert abs(v / (2 * df) - 1) < max(1e-2, 4 * se_v), (df, v)
         p = stats.kstest(row[:200000], stats.chi2(df).cdf).pvalue
         assert p > 0.01, (df, p)
 
@@ -138,26 +146,37 @@ def test_pulse_and_noise_moments_vs_oracle(hip_lib):
 
 
 def test_search_pulse_draws_are_chi2_1(hip_lib):
-    """make_pulses alone (no delay): data / PCHIP(phase) ~ chi2(1)."""
+    """make_pulses alone (no delay): data / PCHIP(phase) ~ chi2(1), on the
+    on-pulse samples of eight seeds pooled (8 x 61 486: one KS test, p >
+    0.01, and the mean).  The device stream is reproduced bit for bit by the
+    NumPy model in tools/philox_model.py, whose 400-seed study of this very
+    statistic (profiles/r03/philox_quality.txt) shows uniform p-values for
+    Philox4x32-7 as for -10."""
     import psrsigsim_amd as pss
     from psrsigsim_amd.signal import FilterBankSignal
     from psrsigsim_amd.pulsar import Pulsar, GaussProfile
-    pss.seed(11)
-    sig = FilterBankSignal(1400, 400, Nsubband=2, fold=False)
-    psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.1, 1))
-    psr.make_pulses(sig, tobs=(1 << 18) * 20.48e-6)
-    x = sig.data.cpu().numpy().astype(np.float64)
-    spp = (sig._samprate_MHz() * 0.005) * 1e6
-    ph = (np.arange(x.shape[1]) / spp) % 1
-    prof = psr.Profiles.calc_profiles(ph)
-    sel = prof[0] > 0.5
-    r = x[0, sel] / prof[0, sel]
-    assert stats.kstest(r[:200000], stats.chi2(1).cdf).pvalue > 0.01
-    assert abs(r.mean() - 1) < 1e-2
+    pooled = []
+    for seed in range(11, 19):
+        pss.seed(seed)
+        sig = FilterBankSignal(1400, 400, Nsubband=2, fold=False)
+        psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.1, 1))
+        psr.make_pulses(sig, tobs=(1 << 18) * 20.48e-6)
+        x = sig.data.cpu().numpy().astype(np.float64)
+        spp = (sig._samprate_MHz() * 0.005) * 1e6
+        ph = (np.arange(x.shape[1]) / spp) % 1
+        prof = psr.Profiles.calc_profiles(ph)
+        sel = prof[0] > 0.5
+        r = x[0, sel] / prof[0, sel]
+        pooled.append(r)
+    r = np.concatenate(pooled)
+    assert stats.kstest(r, stats.chi2(1).cdf).pvalue > 0.01
+    assert abs(r.mean() - 1) < 5e-3
 
 
 def test_radiometer_noise_distribution(hip_lib):
-    """observe(noise=True): (after - before) / norm ~ chi2(df)."""
+    """observe(noise=True): (after - before) / norm ~ chi2(df), df = Nfold =
+    10 (fold mode): 20 s of 2 channels, 195 200 draws, so the 0.5 % bound on
+    the mean is ~5 standard errors (sqrt(2 df / n) / df = 1e-3)."""
     import psrsigsim_amd as pss
     from psrsigsim_amd.signal import FilterBankSignal
     from psrsigsim_amd.pulsar import Pulsar, GaussProfile
@@ -166,7 +185,7 @@ def test_radiometer_noise_distribution(hip_lib):
     pss.seed(12)
     sig = FilterBankSignal(1400, 400, Nsubband=2, sublen=0.05)
     psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
-    psr.make_pulses(sig, tobs=1.0)
+    psr.make_pulses(sig, tobs=20.0)
     before = sig.data.cpu().numpy().astype(np.float64)
     tel = T.Arecibo()
     tel.observe(sig, psr, system="Lband_PUPPI", noise=True)
