@@ -329,7 +329,7 @@ struct Fft {
     // Run the stage list.  Ns = product of the radices already applied.
     template <bool INV, int Ns, int R, int... Rest>
     __device__ static __forceinline__ void run(cf (&v)[E], cf *lds, int tid) {
-        run_impl<INV, false, false, Ns, R, Rest...>(v, lds, tid, nullptr);
+        run_impl<INV, false, false, 0, Ns, R, Rest...>(v, lds, tid, nullptr, nullptr);
     }
     // The same with the radix-16 stage after a radix-16 stage (Ns = 16: the
     // 15 twiddles w^q, w = e^{-+2 pi i k/256}, k < 16) read from the table
@@ -337,7 +337,17 @@ struct Fft {
     // 4 native sincos + 11 products per butterfly.
     template <bool INV, int Ns, int R, int... Rest>
     __device__ static __forceinline__ void run_tw(cf (&v)[E], cf *lds, int tid, const cf *tw16) {
-        run_impl<INV, PSS_TW16 != 0, false, Ns, R, Rest...>(v, lds, tid, tw16);
+        run_impl<INV, PSS_TW16 != 0, false, 0, Ns, R, Rest...>(v, lds, tid, tw16, nullptr);
+    }
+    // run_tw with the last stage's native-sincos twiddles kept in registers:
+    // CM = 1 (forward) saves w^H, w, w^2 .. w^(H-1) (twc[0 .. H-1]) when the
+    // thread has one butterfly per stage (E == R); CM = 2 (inverse, same
+    // thread, the SAME palindromic radix list) takes their conjugates instead
+    // of 4 native sincos and 4 products per butterfly -- the row pass's
+    // inverse after its forward.
+    template <bool INV, int CM, int Ns, int R, int... Rest>
+    __device__ static __forceinline__ void run_tw_c(cf (&v)[E], cf *lds, int tid, const cf *tw16, cf *twc) {
+        run_impl<INV, PSS_TW16 != 0, false, CM, Ns, R, Rest...>(v, lds, tid, tw16, twc);
     }
 
     // Every stage but the last, then the exchange into the last stage's input
@@ -346,11 +356,11 @@ struct Fft {
     template <bool INV, int Ns, int R, int... Rest>
     __device__ static __forceinline__ void run_head_tw(cf (&v)[E], cf *lds, int tid, const cf *tw16) {
         static_assert(sizeof...(Rest) >= 1, "run_head_tw needs at least two stages");
-        run_impl<INV, PSS_TW16 != 0, true, Ns, R, Rest...>(v, lds, tid, tw16);
+        run_impl<INV, PSS_TW16 != 0, true, 0, Ns, R, Rest...>(v, lds, tid, tw16, nullptr);
     }
 
-    template <bool INV, bool TW, bool HEAD, int Ns, int R, int... Rest>
-    __device__ static __forceinline__ void run_impl(cf (&v)[E], cf *lds, int tid, const cf *tw16) {
+    template <bool INV, bool TW, bool HEAD, int CM, int Ns, int R, int... Rest>
+    __device__ static __forceinline__ void run_impl(cf (&v)[E], cf *lds, int tid, const cf *tw16, cf *twc) {
         static_assert(E % R == 0, "E must be a multiple of every radix");
         constexpr int LR = L / R;
 #pragma unroll
@@ -369,23 +379,42 @@ struct Fft {
                 constexpr int H = (R >= 8) ? R / 2 : R;   // powers kept: w^1 .. w^(H-1)
                 cf w[H];
                 const float base = (float)k * (1.0f / (float)(Ns * R));   // [0, 1/R)
+                // twiddle cache (run_tw_c): this stage's powers from the forward pass
+                // (the last stage only: with a palindromic radix list -- the
+                // caller's contract -- it has the same Ns and k in both passes)
+                constexpr bool kCache = CM != 0 && E == R && sizeof...(Rest) == 0 && !(TW && Ns == 16 && R == 16);
 #if defined(PSS_ABLATE) && (PSS_ABLATE & 32)
                 // ablation: twiddles without generation cost (wrong values)
 #pragma unroll
                 for (int q = 1; q < R; ++q) a[q] = cmul(a[q], make_float2(base, (float)q));
                 if (true) { dft<R, INV>(a); continue; }
 #endif
+                if constexpr (kCache && CM == 2) {
 #pragma unroll
-                for (int p2 = 1; p2 < H; p2 *= 2) w[p2] = expi_rev(INV ? p2 * base : -p2 * base);
+                    for (int q = 1; q < H; ++q) w[q] = make_float2(twc[q].x, -twc[q].y);
+                } else {
 #pragma unroll
-                for (int q = 3; q < H; ++q) {
-                    const int hi = 1 << (31 - __builtin_clz(q));   // compile-time after unrolling
-                    if (q != hi) w[q] = cmul(w[hi], w[q - hi]);
+                    for (int p2 = 1; p2 < H; p2 *= 2) w[p2] = expi_rev(INV ? p2 * base : -p2 * base);
+#pragma unroll
+                    for (int q = 3; q < H; ++q) {
+                        const int hi = 1 << (31 - __builtin_clz(q));   // compile-time after unrolling
+                        if (q != hi) w[q] = cmul(w[hi], w[q - hi]);
+                    }
+                    if constexpr (kCache && CM == 1) {
+#pragma unroll
+                        for (int q = 1; q < H; ++q) twc[q] = w[q];
+                    }
                 }
 #pragma unroll
                 for (int q = 1; q < H; ++q) a[q] = cmul(a[q], w[q]);
                 if constexpr (H < R) {
-                    const cf wh = expi_rev(INV ? H * base : -H * base);
+                    cf wh;
+                    if constexpr (kCache && CM == 2) {
+                        wh = make_float2(twc[0].x, -twc[0].y);
+                    } else {
+                        wh = expi_rev(INV ? H * base : -H * base);
+                        if constexpr (kCache && CM == 1) twc[0] = wh;
+                    }
                     a[H] = cmul(a[H], wh);
 #pragma unroll
                     for (int q = 1; q < H; ++q) a[H + q] = cmul(a[H + q], cmul(wh, w[q]));
@@ -428,7 +457,7 @@ struct Fft {
             constexpr int R2 = first<Rest...>();
             load<R2>(v, lds, tid);
             stage_sync<WAVE>();
-            if constexpr (!(HEAD && sizeof...(Rest) == 1)) run_impl<INV, TW, HEAD, Ns * R, Rest...>(v, lds, tid, tw16);
+            if constexpr (!(HEAD && sizeof...(Rest) == 1)) run_impl<INV, TW, HEAD, CM, Ns * R, Rest...>(v, lds, tid, tw16, twc);
         }
     }
 

@@ -15,6 +15,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <math.h>
+#include <type_traits>
 
 #include "pss_device.hpp"
 #include "pss_fft.hpp"
@@ -56,6 +57,11 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 // barriers between stages); experiment switch
 #ifndef PSS_WAVE_COLS
 #define PSS_WAVE_COLS 1
+#endif
+// fast pass C: column blocks per workgroup (2: the two halves of each 128-B
+// output line stored by the same lane back to back; 1: one block); experiment switch
+#ifndef PSS_PC_NBLK
+#define PSS_PC_NBLK 1
 #endif
 // pass A: the four-step twiddle folded into the last column-FFT stage (1) or
 // applied after the FFT (0); experiment switch
@@ -1297,7 +1303,10 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
 #pragma unroll
                 for (int q = 0; q < RF0; ++q) v[ib * RF0 + q] = Y.ld2(off, q * kQS);
             }
-            if constexpr (!(kAbl & 2)) FF::template run_tw<false, 1, F...>(v, lds, tid, tw16);
+            // the last stage's twiddles kept for the inverse (palindromic radix lists)
+            constexpr int kTwc = std::is_same<RList<F...>, RList<I...>>::value ? 2 : 0;
+            cf twc[8];
+            if constexpr (!(kAbl & 2)) FF::template run_tw_c<false, kTwc ? 1 : 0, 1, F...>(v, lds, tid, tw16, twc);
             FF::template store<RFL>(v, lds, tid);
             __syncthreads();
             // pair ramp factors (k_pair_tab): {E, D} per q, wave-uniform
@@ -1367,7 +1376,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                 }
             }
             __syncthreads();
-            if constexpr (!(kAbl & 2)) FF::template run_tw<true, 1, I...>(v, lds, tid, tw16);
+            if constexpr (!(kAbl & 2)) FF::template run_tw_c<true, kTwc, 1, I...>(v, lds, tid, tw16, twc);
 #pragma unroll
             for (int ib = 0; ib < E / RF0; ++ib) {
                 const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
@@ -1809,20 +1818,25 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     // positions a delayed null's mask table marks for its channel (PSS_FUSE_NULL),
     // as replacement + noise; with PSS_FUSE_NULL=0 those are rewritten
     // afterwards by k_null_fix_list instead.
+    // NBLK adjacent column blocks per workgroup, one after the other through
+    // the same LDS, their outputs held in registers and stored together: the
+    // two 64-B halves of every 128-B output line (16 columns x 4 B per
+    // channel row) leave the same lane in back-to-back stores instead of from
+    // two workgroups (whose halves do not always meet in L2: PMC writes were
+    // 1.11x the algorithmic bytes with NBLK = 1).
+    template <int NBLK = 1>
     __device__ static void passC_fast(const KP &k) {
         static_assert(kItemsExact, "fast pass C: whole items per thread");
         __shared__ __align__(16) cf lds[B * LdsC::RS];
         const int tid = threadIdx.x;
-        int cbx, pr;
-        xcd_block(cbx, pr);
+        int cbx2, pr;
+        xcd_block(cbx2, pr);
         const int ra = 2 * pr - k.poff, rb = ra + 1;
         const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
-        const int64_t n20 = (int64_t)cbx * B;
         const int64_t N2 = k.N2;
         const PssPipeline &p = k.p;
         const float invN = k.invN, nn = p.noise_norm;
         const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
-        inv_block(k, k.Yd + (int64_t)pr * pstride(k), n20, lds, tid);
         const Rng gn(p.seed, p.call_noise, P_NOISE);
         // fused delayed null (kFuseNull): the channels' table splits
         const bool mnull = kFuseNull && k.mtab;
@@ -1836,47 +1850,53 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         const float sc = p.null_rep_scale;
         const uint32_t rbytes = (uint32_t)(k.N * 4);
         const Buf oa(p.data + (int64_t)max(ra, 0) * p.ld, rbytes), ob(p.data + (int64_t)min(rb, p.nchan - 1) * p.ld, rbytes);
-        float acc[ITEMS][2][4];
+        float acc[NBLK][ITEMS][2][4];
 #pragma unroll
-        for (int t = 0; t < ITEMS; ++t) {
-            const int it = tid + t * T;
-            const int n1 = it / (B / 4);
-            const int b4 = (it - n1 * (B / 4)) * 4;
-            const uint32_t n = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4;   // N <= 2^24
-            float4 xa, xb;
-            if constexpr (kAbl & 1) {
-                const float fn = (float)n;
-                xa = make_float4(fn, fn + 1.f, fn + 2.f, fn + 3.f);
-                xb = make_float4(fn, fn - 1.f, fn - 2.f, fn - 3.f);
-            } else {
-                xa = chi2_1x4(gn.bits(n >> 2, ca, 0u));
-                xb = chi2_1x4(gn.bits(n >> 2, cb, 0u));
-            }
-            const float na[4] = {xa.x, xa.y, xa.z, xa.w}, nb[4] = {xb.x, xb.y, xb.z, xb.w};
+        for (int blk = 0; blk < NBLK; ++blk) {
+            const int64_t n20 = (int64_t)(cbx2 * NBLK + blk) * B;
+            if (blk) __syncthreads();            // the previous block's epilogue has read LDS
+            inv_block(k, k.Yd + (int64_t)pr * pstride(k), n20, lds, tid);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const cf z = lds[LdsC::at(b4 + i, n1)];
-                acc[t][0][i] = fmaf(nn, na[i], z.x * invN);
-                acc[t][1][i] = fmaf(nn, nb[i], z.y * invN);
-            }
-            if (mnull) {
-                // nulled samples: replacement + noise, the draws and
-                // expression of epilogue4 / k_null_fix_list (bitwise equal)
-                const uint32_t ha = hasa ? mask_hits4(k, (int64_t)n, isa, tma) : 0u;
-                const uint32_t hb = hasb ? mask_hits4(k, (int64_t)n, isb, tmb) : 0u;
-                if (ha) {
-                    const float4 r = chi2_1x4(gr.bits(n >> 2, ca, 0u));
-                    const float vr[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if ((ha >> i) & 1u) acc[t][0][i] = fmaf(nn, na[i], vr[i] * sc);
+            for (int t = 0; t < ITEMS; ++t) {
+                const int it = tid + t * T;
+                const int n1 = it / (B / 4);
+                const int b4 = (it - n1 * (B / 4)) * 4;
+                const uint32_t n = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4;   // N <= 2^24
+                float4 xa, xb;
+                if constexpr (kAbl & 1) {
+                    const float fn = (float)n;
+                    xa = make_float4(fn, fn + 1.f, fn + 2.f, fn + 3.f);
+                    xb = make_float4(fn, fn - 1.f, fn - 2.f, fn - 3.f);
+                } else {
+                    xa = chi2_1x4(gn.bits(n >> 2, ca, 0u));
+                    xb = chi2_1x4(gn.bits(n >> 2, cb, 0u));
                 }
-                if (hb) {
-                    const float4 r = chi2_1x4(gr.bits(n >> 2, cb, 0u));
-                    const float vr[4] = {r.x, r.y, r.z, r.w};
+                const float na[4] = {xa.x, xa.y, xa.z, xa.w}, nb[4] = {xb.x, xb.y, xb.z, xb.w};
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        if ((hb >> i) & 1u) acc[t][1][i] = fmaf(nn, nb[i], vr[i] * sc);
+                for (int i = 0; i < 4; ++i) {
+                    const cf z = lds[LdsC::at(b4 + i, n1)];
+                    acc[blk][t][0][i] = fmaf(nn, na[i], z.x * invN);
+                    acc[blk][t][1][i] = fmaf(nn, nb[i], z.y * invN);
+                }
+                if (mnull) {
+                    // nulled samples: replacement + noise, the draws and
+                    // expression of epilogue4 / k_null_fix_list (bitwise equal)
+                    const uint32_t ha = hasa ? mask_hits4(k, (int64_t)n, isa, tma) : 0u;
+                    const uint32_t hb = hasb ? mask_hits4(k, (int64_t)n, isb, tmb) : 0u;
+                    if (ha) {
+                        const float4 r = chi2_1x4(gr.bits(n >> 2, ca, 0u));
+                        const float vr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            if ((ha >> i) & 1u) acc[blk][t][0][i] = fmaf(nn, na[i], vr[i] * sc);
+                    }
+                    if (hb) {
+                        const float4 r = chi2_1x4(gr.bits(n >> 2, cb, 0u));
+                        const float vr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            if ((hb >> i) & 1u) acc[blk][t][1][i] = fmaf(nn, nb[i], vr[i] * sc);
+                    }
                 }
             }
         }
@@ -1885,15 +1905,25 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             const int it = tid + t * T;
             const int n1 = it / (B / 4);
             const int b4 = (it - n1 * (B / 4)) * 4;
-            const uint32_t off = ((uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4) * 4u;
-            if constexpr (kAbl & 64) {   // ablation: contiguous stores (wrong place)
-                const uint32_t o2 = ((uint32_t)(cbx * T * ITEMS) + (uint32_t)it) * 16u;
-                if (hasa) oa.st4(acc[t][0][0], acc[t][0][1], acc[t][0][2], acc[t][0][3], o2, 0);
-                if (hasb) ob.st4(acc[t][1][0], acc[t][1][1], acc[t][1][2], acc[t][1][3], o2, 0);
-                continue;
+#pragma unroll
+            for (int blk = 0; blk < NBLK; ++blk) {
+                const int64_t n20 = (int64_t)(cbx2 * NBLK + blk) * B;
+                const uint32_t off = ((uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4) * 4u;
+                if constexpr (kAbl & 64) {   // ablation: contiguous stores (wrong place)
+                    const uint32_t o2 = ((uint32_t)((cbx2 * NBLK + blk) * T * ITEMS) + (uint32_t)it) * 16u;
+                    if (hasa) oa.st4(acc[blk][t][0][0], acc[blk][t][0][1], acc[blk][t][0][2], acc[blk][t][0][3], o2, 0);
+                    if (hasb) ob.st4(acc[blk][t][1][0], acc[blk][t][1][1], acc[blk][t][1][2], acc[blk][t][1][3], o2, 0);
+                    continue;
+                }
+                if (hasa) oa.st4<PSS_OUT_AUX>(acc[blk][t][0][0], acc[blk][t][0][1], acc[blk][t][0][2], acc[blk][t][0][3], off, 0);
             }
-            if (hasa) oa.st4<PSS_OUT_AUX>(acc[t][0][0], acc[t][0][1], acc[t][0][2], acc[t][0][3], off, 0);
-            if (hasb) ob.st4<PSS_OUT_AUX>(acc[t][1][0], acc[t][1][1], acc[t][1][2], acc[t][1][3], off, 0);
+#pragma unroll
+            for (int blk = 0; blk < NBLK; ++blk) {
+                if constexpr (kAbl & 64) continue;
+                const int64_t n20 = (int64_t)(cbx2 * NBLK + blk) * B;
+                const uint32_t off = ((uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4) * 4u;
+                if (hasb) ob.st4<PSS_OUT_AUX>(acc[blk][t][1][0], acc[blk][t][1][1], acc[blk][t][1][2], acc[blk][t][1][3], off, 0);
+            }
         }
     }
 
@@ -1931,8 +1961,8 @@ template <typename C, int T, bool SHARED>
 __global__ __launch_bounds__(T) void k_pairA_fast(KP k) { C::template passA<true, SHARED>(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairC(KP k) { C::passC(k); }
-template <typename C, int T>
-__global__ __launch_bounds__(T) void k_pairC_fast(KP k) { C::passC_fast(k); }
+template <typename C, int T, int NBLK>
+__global__ __launch_bounds__(T) void k_pairC_fast(KP k) { C::template passC_fast<NBLK>(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_node_col(KP k, float *nodes) { C::node_col(k, nodes); }
 
@@ -2944,7 +2974,15 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     tk_begin(TK_COLC, st);
     if (fast) {
         if constexpr (PCC::kItemsExact)
-            k_pairC_fast<PCC, TC><<<dim3((unsigned)(N2 / BC), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
+        {
+            // PSS_PC_NBLK = 2: two adjacent column blocks per workgroup
+            // (rejected from the ISA, not run: block 0's 32 output registers stay live
+            // through block 1 and the kernel spills 31 VGPRs at the 128 cap)
+            if constexpr (PSS_PC_NBLK == 2 && (N2 / BC) % 2 == 0)
+                k_pairC_fast<PCC, TC, 2><<<dim3((unsigned)(N2 / BC / 2), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
+            else
+                k_pairC_fast<PCC, TC, 1><<<dim3((unsigned)(N2 / BC), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
+        }
     } else {
         k_pairC<PC, T><<<gc, dim3(T), 0, st>>>(k);
     }
