@@ -70,6 +70,11 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 #endif
 // delayed-null fix-up over the list of table words with nulls (1) or over
 // every word of every channel (0); experiment switch
+// row pass: keep the last forward stage's twiddles in registers for the
+// inverse (experiment switch)
+#ifndef PSS_ROW_TWC
+#define PSS_ROW_TWC 0
+#endif
 #ifndef PSS_NULL_LIST
 #define PSS_NULL_LIST 1
 #endif
@@ -1304,7 +1309,10 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                 for (int q = 0; q < RF0; ++q) v[ib * RF0 + q] = Y.ld2(off, q * kQS);
             }
             // the last stage's twiddles kept for the inverse (palindromic radix lists)
-            constexpr int kTwc = std::is_same<RList<F...>, RList<I...>>::value ? 2 : 0;
+            // (PSS_ROW_TWC: off by default -- its 16 live VGPRs across the ramp
+            // push the 4096-point kernel past the 128-VGPR cap of 4 waves per
+            // SIMD, and it measured neutral, profiles/r03/s3)
+            constexpr int kTwc = (PSS_ROW_TWC && std::is_same<RList<F...>, RList<I...>>::value) ? 2 : 0;
             cf twc[8];
             if constexpr (!(kAbl & 2)) FF::template run_tw_c<false, kTwc ? 1 : 0, 1, F...>(v, lds, tid, tw16, twc);
             FF::template store<RFL>(v, lds, tid);
@@ -1314,48 +1322,30 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
             const uint64_t hsum = (rwa >> 1) + (rwb >> 1), hdif = (rwa >> 1) - (rwb >> 1);
 #pragma unroll
             for (int ib = 0; ib < E / RFL; ++ib) {
-                const int jg = tid + ib * T, b = jg / LRL, jj = jg - b * LRL;
+                const int jg = tid + ib * T;
+                // row side b is wave-uniform when LRL is a multiple of the
+                // wave: say so, so the mirror-read choice below is a scalar branch
+                const int b = (LRL % 64 == 0) ? __builtin_amdgcn_readfirstlane(jg / LRL) : jg / LRL;
+                const int jj = jg - b * LRL;
                 const int row = b ? rowB : rowA;
                 const int64_t kb0 = row + (int64_t)N1 * jj;
                 const cf bE = expi_rev(-fix_to_rev((uint64_t)kb0 * hsum));
                 const cf bD = expi_rev(-fix_to_rev((uint64_t)kb0 * hdif));
-                // mirror bins k2m = N2 - 1 - k2 = P0 - q LRL (all but row 0 of
-                // the {0, N1/2} pair, whose bin 0 pairs with itself): with
-                // LRL % 256 == 0 the swizzle XOR is the same for every q, so
-                // the reads are one byte base minus immediate offsets
-                constexpr bool kMirXB = FF::XB && (LRL % 256 == 0);
-                const bool affine = !(j == 0 && row == 0);       // wave-uniform
-                uint32_t mbase = 0;
-                if constexpr (kMirXB) mbase = lds_byte(lds) + 8u * (uint32_t)LD::at(j == 0 ? b : 1 - b, N2 - 1 - jj);
-#pragma unroll
-                for (int q = 0; q < RFL; ++q) {
-                    const int i = ib * RFL + q, k2 = jj + q * LRL;
-                    cf Zm;
-                    if (kMirXB && affine) {
-                        Zm = lds_ld(mbase - 8u * (uint32_t)(q * LRL));
-                    } else {
-                        int bm, k2m;
-                        if (j == 0) { bm = b; k2m = (row == 0) ? ((N2 - k2) & (N2 - 1)) : (N2 - 1 - k2); }
-                        else        { bm = 1 - b; k2m = N2 - 1 - k2; }
-                        Zm = lds[LD::at(bm, k2m)];
-                    }
+                const bool dc = (kb0 == 0);                      // one lane of one wave per launch
+                // bin q of this butterfly from Z = v[i] and its mirror Zm:
+                // W = D_a R_a + i D_b R_b; DC (q = 0) and Nyquist (q = RFL/2)
+                // of kb0 = 0 by select (no per-bin branch: the body stays
+                // straight-line, so the mirror reads of several bins are in
+                // flight together)
+                auto bin = [&](int q, cf Zm) {
+                    const int i = ib * RFL + q;
                     const cf Z = v[i];
                     // 2 D_a and 2 D_b (DC / Nyquist and the tail extension)
                     const cf Sa = make_float2(Z.x + Zm.x, Z.y - Zm.y);
                     const cf Sb = make_float2(Z.y + Zm.y, Zm.x - Z.x);
+                    cf W;
                     if constexpr (kAbl & 8) {
-                        v[i] = cadd(Sa, Sb);
-                    } else if (kb0 == 0 && 2 * q == RFL) {          // Nyquist bin
-                        float fa = k.p.nyq_re[ra], fb = k.p.nyq_re[rb];
-                        if constexpr (TAIL) {                       // H(N/2) = (1-a)/(1+a)
-                            const float ta = k.p.tail_a[ra], tb = k.p.tail_a[rb];
-                            fa *= (1.0f - ta) / (1.0f + ta);
-                            fb *= (1.0f - tb) / (1.0f + tb);
-                        }
-                        v[i] = make_float2((0.5f * Sa.x) * fa, (0.5f * Sb.x) * fb);
-                    } else if (kb0 == 0 && q == 0) {                // DC (H = 1)
-                        const cf Da = make_float2(0.5f * Sa.x, 0.5f * Sa.y), Db = make_float2(0.5f * Sb.x, 0.5f * Sb.y);
-                        v[i] = make_float2(Da.x - Db.y, Da.y + Db.x);
+                        W = cadd(Sa, Sb);
                     } else {
                         const cf Ef = cmul(bE, ptab[2 * q]), Df = cmul(bD, ptab[2 * q + 1]);
                         if constexpr (TAIL) {
@@ -1365,13 +1355,49 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                             const cf rb_ = cmul(make_float2(0.5f * Ef.x, 0.5f * Ef.y), cmul_conj(tail_factor(k.p.tail_a[rb], w), Df));
                             const cf A = cmul(Sa, ra_);
                             const cf Bv = cmul(Sb, rb_);
-                            v[i] = make_float2(A.x - Bv.y, A.y + Bv.x);
+                            W = make_float2(A.x - Bv.y, A.y + Bv.x);
                         } else {
                             // W = E (Z cos d - i conj(Zm) sin d), D = cos d - i sin d
                             const float c = Df.x, s = -Df.y;
                             const cf in = make_float2(fmaf(Z.x, c, -(Zm.y * s)), fmaf(Z.y, c, -(Zm.x * s)));
-                            v[i] = cmul(Ef, in);
+                            W = cmul(Ef, in);
                         }
+                        if (2 * q == RFL) {                         // Nyquist bin (compile-time q)
+                            float fa = k.p.nyq_re[ra], fb = k.p.nyq_re[rb];
+                            if constexpr (TAIL) {                   // H(N/2) = (1-a)/(1+a)
+                                const float ta = k.p.tail_a[ra], tb = k.p.tail_a[rb];
+                                fa *= (1.0f - ta) / (1.0f + ta);
+                                fb *= (1.0f - tb) / (1.0f + tb);
+                            }
+                            const cf Wn = make_float2((0.5f * Sa.x) * fa, (0.5f * Sb.x) * fb);
+                            W = dc ? Wn : W;
+                        } else if (q == 0) {                        // DC (H = 1)
+                            const cf Da = make_float2(0.5f * Sa.x, 0.5f * Sa.y), Db = make_float2(0.5f * Sb.x, 0.5f * Sb.y);
+                            const cf Wd = make_float2(Da.x - Db.y, Da.y + Db.x);
+                            W = dc ? Wd : W;
+                        }
+                    }
+                    v[i] = W;
+                };
+                // mirror bins k2m = N2 - 1 - k2 = P0 - q LRL (all but row 0 of
+                // the {0, N1/2} pair, whose bin 0 pairs with itself): with
+                // LRL % 256 == 0 the swizzle XOR is the same for every q, so
+                // the reads are one byte base minus immediate offsets.  The
+                // choice is one scalar branch around the whole bin loop.
+                constexpr bool kMirXB = FF::XB && (LRL % 256 == 0);
+                const bool affine = !(j == 0 && row == 0);       // wave-uniform
+                if (kMirXB && affine) {
+                    const uint32_t mbase = lds_byte(lds) + 8u * (uint32_t)LD::at(j == 0 ? b : 1 - b, N2 - 1 - jj);
+#pragma unroll
+                    for (int q = 0; q < RFL; ++q) bin(q, lds_ld(mbase - 8u * (uint32_t)(q * LRL)));
+                } else {
+#pragma unroll
+                    for (int q = 0; q < RFL; ++q) {
+                        const int k2 = jj + q * LRL;
+                        int bm, k2m;
+                        if (j == 0) { bm = b; k2m = (row == 0) ? ((N2 - k2) & (N2 - 1)) : (N2 - 1 - k2); }
+                        else        { bm = 1 - b; k2m = N2 - 1 - k2; }
+                        bin(q, lds[LD::at(bm, k2m)]);
                     }
                 }
             }
