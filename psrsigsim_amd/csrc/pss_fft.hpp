@@ -125,6 +125,105 @@ __device__ __forceinline__ void dft(cf *a) {
     }
 }
 
+// --------------------------------------------------------------------------
+// Register-resident DFT of a short mixed-radix length (the fold-mode
+// four-step's columns, N1 in {6, 10, 12, 20, 24, 30, 40, 48, 60}): one thread
+// holds a whole column, so the transform needs no LDS exchange at all.
+// Decimation in time, N = R M (R = 4, 2, 3 or 5): the R decimated
+// subsequences x[R m + r] are transformed recursively, then for every k < M
+// the radix-R butterfly over r of W_N^{r k} Y_r[k] gives X[k + M q].  With
+// full unrolling every twiddle is a compile-time constant (cx_cospi below:
+// double-precision Taylor series evaluated by the compiler, rounded once to
+// fp32; exact 0 / +-1 at multiples of pi/2).
+// --------------------------------------------------------------------------
+constexpr double cx_pi = 3.14159265358979323846;
+// cos(pi x) for x in [-1, 1] by range reduction to [-1/4, 1/4] and Taylor series
+constexpr double cx_cospi_red(double x, bool sin_form) {
+    const double t = cx_pi * x, t2 = t * t;
+    double s = 0.0, term = sin_form ? t : 1.0;
+    for (int n = 0; n < 14; ++n) {
+        s += term;
+        const int a = sin_form ? 2 * n + 2 : 2 * n + 1, b = a + 1;
+        term *= -t2 / ((double)a * (double)b);
+    }
+    return s;
+}
+constexpr double cx_cospi(double x) {
+    // x -> [0, 2), then the octant
+    while (x < 0.0) x += 2.0;
+    while (x >= 2.0) x -= 2.0;
+    if (x > 1.0) x = 2.0 - x;                          // cos(pi x) even about 1
+    if (x == 0.5) return 0.0;
+    if (x == 0.0) return 1.0;
+    if (x == 1.0) return -1.0;
+    if (x <= 0.25) return cx_cospi_red(x, false);
+    if (x <= 0.75) return cx_cospi_red(0.5 - x, true);   // cos(pi x) = sin(pi (1/2 - x))
+    return -cx_cospi_red(1.0 - x, false);
+}
+constexpr double cx_sinpi(double x) { return cx_cospi(x - 0.5); }
+
+// W_N^k x = e^{-+2 pi i k / N} x with a compile-time k (forward: minus)
+template <int N, int K, bool INV>
+__device__ __forceinline__ cf rot_n(cf x) {
+    constexpr int k = ((K % N) + N) % N;
+    if constexpr (k == 0) {
+        return x;
+    } else if constexpr (4 * k == N) {
+        return INV ? make_float2(-x.y, x.x) : make_float2(x.y, -x.x);
+    } else if constexpr (2 * k == N) {
+        return make_float2(-x.x, -x.y);
+    } else if constexpr (4 * k == 3 * N) {
+        return INV ? make_float2(x.y, -x.x) : make_float2(-x.y, x.x);
+    } else {
+        constexpr float c = (float)cx_cospi(2.0 * k / N);
+        constexpr float s = (float)cx_sinpi(2.0 * k / N);
+        return cmul(x, make_float2(c, INV ? s : -s));
+    }
+}
+
+template <int N, bool INV>
+struct RegDft {
+    static constexpr int R = (N % 4 == 0 && N > 4) ? 4 : (N % 2 == 0) ? 2 : (N % 3 == 0) ? 3 : 5;
+    static constexpr int M = N / R;
+    // y[k + M q] = sum_r W_N^{r k} W_R^{r q} (DFT_M x[R m + r])[k]
+    template <int K, int Q>
+    __device__ static __forceinline__ void comb(cf (&s)[R][M], cf (&x)[N]) {
+        if constexpr (K < M) {
+            cf t[R];
+            twr<K, 0>(s, t);
+            dft<R, INV>(t);
+#pragma unroll
+            for (int q = 0; q < R; ++q) x[K + M * q] = t[q];
+            comb<K + 1, 0>(s, x);
+        }
+    }
+    template <int K, int RR>
+    __device__ static __forceinline__ void twr(cf (&s)[R][M], cf (&t)[R]) {
+        if constexpr (RR < R) {
+            t[RR] = rot_n<N, RR * K, INV>(s[RR][K]);
+            twr<K, RR + 1>(s, t);
+        }
+    }
+    __device__ static __forceinline__ void run(cf (&x)[N]) {
+        if constexpr (N == 2 || N == 3 || N == 4 || N == 5) {
+            dft<N, INV>(x);
+        } else {
+            cf s[R][M];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int m = 0; m < M; ++m) s[r][m] = x[R * m + r];
+#pragma unroll
+            for (int r = 0; r < R; ++r) RegDft<M, INV>::run(s[r]);
+            comb<0, 0>(s, x);
+        }
+    }
+};
+template <bool INV>
+struct RegDft<1, INV> {
+    __device__ static __forceinline__ void run(cf (&)[1]) {}
+};
+
 // LDS layout of BATCH sequences of length L.  L % 16 == 0: position p of a
 // row lives at p ^ ((p >> 4) & 15) -- an XOR swizzle inside each aligned
 // 16-complex block, so the stride-16 Stockham scatters spread over the banks
@@ -140,7 +239,9 @@ template <int L, int XRS = 1>
 struct Lds {
     // XRS < 0: the padded layout (a kernel whose accesses it suits better)
     static constexpr bool SWZ = (L % 16) == 0 && !PSS_LDS_PAD && XRS >= 0;
-    static constexpr int RS = SWZ ? L + XRS : L + L / 16 + 1;   // row pitch (complex)
+    // row pitch (complex); the padded pitch is odd so that accesses across
+    // rows (one position of many sequences) spread over the banks
+    static constexpr int RS = SWZ ? L + XRS : ((L + L / 16 + 1) | 1);
     __device__ static __forceinline__ int at(int b, int p) {
         if constexpr (SWZ) return b * RS + (p ^ ((p >> 4) & 15));
         else return b * RS + p + (p >> 4);

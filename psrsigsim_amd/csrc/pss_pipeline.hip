@@ -572,6 +572,15 @@ __device__ __forceinline__ uint32_t mask_bits4(const KP &k, int r, int cbx, int 
 // contiguous (wrong-place) stores would take 14.3 ms -- the residual cost of
 // the strided output is ~4 ms.  Non-temporal / sc1 loads of the spill make it
 // worse (21-25 ms): neighbouring blocks share the spill's lines through L2.
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
 __device__ __forceinline__ void xcd_block(int &bx, int &by) {
     const uint32_t gx = gridDim.x, total = gx * gridDim.y;
     const uint32_t id = blockIdx.x + blockIdx.y * gx;
@@ -1481,6 +1490,12 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     // the unrolled fast kernels need a whole number of 4-sample items per
     // thread (N1 = 2^m); the generic ones loop (any N1, e.g. 30 = 2 * 3 * 5)
     static constexpr bool kItemsExact = ITEMS * 4 * T == N1 * B;
+    // Mixed-radix columns (N1 not a power of two, one column per thread, B
+    // == T): the column DFTs run in registers (RegDft: compile-time twiddles,
+    // no LDS exchange), the spill is written / read one column per lane
+    // (consecutive lanes = consecutive columns: coalesced rows)
+    static constexpr bool kRegCols = (B == T) && ((N1 & (N1 - 1)) != 0);
+    static constexpr int kFoldWaves = N1 <= 30 ? 4 : 2;      // min waves per SIMD of the fold kernels
     static_assert(B % 4 == 0, "4-sample items");
 
     // A: generate channels a, b into z = d_a + i d_b; column FFTs; twiddle; spill.
@@ -1611,6 +1626,13 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             for (int i = 0; i < 4; ++i) lds[LdsC::at(b4 + i, n1)] = make_float2(xa[i], xb[i]);
         }
         __syncthreads();
+        if constexpr (kRegCols) {
+            cf x[N1];
+#pragma unroll
+            for (int n1 = 0; n1 < N1; ++n1) x[n1] = lds[LdsC::at(tid, n1)];
+            reg_spill(k, x, pr, n20 + tid);
+            return;
+        }
         cf v[E];
         const float invN = k.invN;
         if constexpr (kWaveCols) {
@@ -1711,6 +1733,129 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                 dst[0] = make_float4(a0.x, a0.y, a1.x, a1.y);
                 dst[1] = make_float4(a2.x, a2.y, a3.x, a3.y);
             }
+        }
+    }
+
+    // Register columns (kRegCols): forward DFT of this thread's column n2
+    // (x[n1] = z(n1 N2 + n2)), four-step twiddle W_N^{n2 k1}, spill row k1
+    // at column n2.
+    __device__ static __forceinline__ void reg_spill(const KP &k, cf (&x)[N1], int pr, int64_t n2) {
+        static_assert(kRegCols, "register columns only");
+        RegDft<N1, false>::run(x);
+        const Buf Y(k.Yd + (int64_t)pr * pstride(k), (uint32_t)(pstride(k) * 8));
+        const uint32_t RP = (uint32_t)rpitch(k);
+        const float invN = k.invN;
+#pragma unroll
+        for (int k1 = 0; k1 < N1; ++k1) {
+            // n2 k1 < N (exact in 32-bit and in float)
+            float rev = (float)((uint32_t)n2 * (uint32_t)k1) * invN;
+            if (rev >= 0.5f) rev -= 1.0f;
+            const cf w = k1 ? cmul(x[k1], expi_rev(-rev)) : x[k1];
+            Y.st2(w, ((uint32_t)k1 * RP + (uint32_t)n2) * 8u, 0u);
+        }
+    }
+    // ... and back: spill column n2 times W_N^{-n2 k1}, inverse DFT
+    // (unscaled), x[n1] = z(n1 N2 + n2) N.
+    __device__ static __forceinline__ void reg_unspill(const KP &k, cf (&x)[N1], int pr, int64_t n2) {
+        static_assert(kRegCols, "register columns only");
+        const Buf Y(k.Yd + (int64_t)pr * pstride(k), (uint32_t)(pstride(k) * 8));
+        const uint32_t RP = (uint32_t)rpitch(k);
+        const float invN = k.invN;
+#pragma unroll
+        for (int k1 = 0; k1 < N1; ++k1) x[k1] = Y.ld2(((uint32_t)k1 * RP + (uint32_t)n2) * 8u, 0u);
+#pragma unroll
+        for (int k1 = 1; k1 < N1; ++k1) {
+            float rev = (float)((uint32_t)n2 * (uint32_t)k1) * invN;
+            if (rev >= 0.5f) rev -= 1.0f;
+            x[k1] = cmul(x[k1], expi_rev(rev));
+        }
+        RegDft<N1, true>::run(x);
+    }
+
+    // Fold-mode fast passes (host-selected on the mixed-radix split: fold
+    // source, chi2(df != 1) draws by the pair sampler, no injected draws, no
+    // null in the epilogue).  Every lane owns one column n2 = n20 + lane and
+    // keeps it in registers from the draws to the spill: no LDS at all.  The
+    // pair sampler keys samples (2m, 2m + 1) -- columns (n2 & ~1, n2 | 1) of
+    // one row -- so the lanes of a column pair split the draws by channel
+    // (even lane: channel a, odd lane: channel b, both columns) and swap the
+    // halves with one DPP move: every draw once, bitwise the values
+    // source4 / epilogue4 produce (test_gpu_configs: fold fast == generic).
+    __device__ static __forceinline__ void pair_draws(const Rng &g, uint32_t n, uint32_t cme, bool odd, float df,
+                                                      float &va, float &vb) {
+        float x0, x1;
+        chi2_pair(g, n >> 1, cme, df, x0, x1);
+        const float send = odd ? x0 : x1;          // even: a(n2 | 1); odd: b(n2 & ~1)
+        const float recv = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0xB1, 0xF, 0xF, false));
+        va = odd ? recv : x0;
+        vb = odd ? x1 : recv;
+    }
+    __device__ static void passA_fold(const KP &k) {
+        static_assert(kRegCols, "fold fast pass A: register columns");
+        const int tid = threadIdx.x;
+        int cbx, pr;
+        xcd_block(cbx, pr);
+        const int ra = 2 * pr - k.poff, rb = ra + 1;
+        const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
+        const PssPipeline &p = k.p;
+        const uint32_t n2 = (uint32_t)(cbx * B + tid), N2 = (uint32_t)k.N2;
+        const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
+        const bool odd = (tid & 1) != 0;
+        const Rng g(p.seed, p.call_gen, P_PULSE);
+        const int last = p.prof_rows - 1;
+        const int pra = (p.prof_rows == 1) ? 0 : min(max((int)ca - p.prof_row0, 0), last);
+        const int prb = (p.prof_rows == 1) ? 0 : min(max((int)cb - p.prof_row0, 0), last);
+        const float *pfa = p.prof + (int64_t)pra * p.nph, *pfb = p.prof + (int64_t)prb * p.nph;
+        const uint32_t nph = (uint32_t)p.nph;
+        const float dn = p.draw_norm, df = p.gen_df;
+        cf x[N1];
+        uint32_t b = n2 % nph;                       // profile bin of sample n1 N2 + n2
+        const uint32_t db = N2 % nph;
+        // (compile-time row index: a runtime-indexed x[] would live in scratch)
+        static_for<0, N1>([&](auto IC) {
+            constexpr int n1 = decltype(IC)::value;
+            const uint32_t n = (uint32_t)n1 * N2 + n2;
+            float va, vb;
+            pair_draws(g, n, odd ? cb : ca, odd, df, va, vb);
+            x[n1] = make_float2(hasa ? pfa[b] * va * dn : 0.f, hasb ? pfb[b] * vb * dn : 0.f);
+            b += db;
+            if (b >= nph) b -= nph;
+        });
+        reg_spill(k, x, pr, n2);
+    }
+    __device__ static void passC_fold(const KP &k) {
+        static_assert(kRegCols, "fold fast pass C: register columns");
+        const int tid = threadIdx.x;
+        int cbx, pr;
+        xcd_block(cbx, pr);
+        const int ra = 2 * pr - k.poff, rb = ra + 1;
+        const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
+        const PssPipeline &p = k.p;
+        const uint32_t n2 = (uint32_t)(cbx * B + tid), N2 = (uint32_t)k.N2;
+        const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
+        const bool odd = (tid & 1) != 0;
+        const Rng g(p.seed, p.call_noise, P_NOISE);
+        const float invN = k.invN, nn = p.noise_norm, df = p.noise_df;
+        // The scaled column is staged in LDS, private to the lane (no
+        // barrier): the noise loop may call the rare Marsaglia-Tsang retry,
+        // and a whole column held in registers across those calls spills
+        // (167 VGPRs of scratch at N1 = 30).
+        __shared__ cf sg[N1 * B];                       // [n1][lane]
+        {
+            cf x[N1];
+            reg_unspill(k, x, pr, n2);
+#pragma unroll
+            for (int n1 = 0; n1 < N1; ++n1) sg[n1 * B + tid] = make_float2(x[n1].x * invN, x[n1].y * invN);
+        }
+        float *oa = p.data + (int64_t)max(ra, 0) * p.ld, *ob = p.data + (int64_t)min(rb, p.nchan - 1) * p.ld;
+#pragma unroll 2
+        for (int n1 = 0; n1 < N1; ++n1) {
+            const uint32_t n = (uint32_t)n1 * N2 + n2;
+            float va, vb;
+            pair_draws(g, n, odd ? cb : ca, odd, df, va, vb);
+            const cf z = sg[n1 * B + tid];
+            if (hasa) oa[n] = fmaf(nn, va, z.x);
+            if (hasb) ob[n] = fmaf(nn, vb, z.y);
         }
     }
 
@@ -1815,7 +1960,15 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         const int64_t n20 = (int64_t)cbx * B;
         const bool mask = k.mtab != 0;
         const float invN = k.invN;
-        inv_block(k, k.Yd + (int64_t)pr * pstride(k), n20, lds, tid);
+        if constexpr (kRegCols) {
+            cf x[N1];
+            reg_unspill(k, x, pr, n20 + tid);
+#pragma unroll
+            for (int n1 = 0; n1 < N1; ++n1) lds[LdsC::at(tid, n1)] = x[n1];
+            __syncthreads();
+        } else {
+            inv_block(k, k.Yd + (int64_t)pr * pstride(k), n20, lds, tid);
+        }
 #pragma unroll 1
         for (int it = tid; it < N1 * B / 4; it += T) {
             const int n1 = it / (B / 4);
@@ -1991,6 +2144,12 @@ template <typename C, int T, int NBLK>
 __global__ __launch_bounds__(T) void k_pairC_fast(KP k) { C::template passC_fast<NBLK>(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_node_col(KP k, float *nodes) { C::node_col(k, nodes); }
+// (4 waves per SIMD for columns up to 30: the compiler would otherwise keep
+// every row's draws in flight at once, 210 VGPRs for N1 = 30)
+template <typename C, int T>
+__global__ __launch_bounds__(T, C::kFoldWaves) void k_pairA_fold(KP k) { C::passA_fold(k); }
+template <typename C, int T>
+__global__ __launch_bounds__(T, C::kFoldWaves) void k_pairC_fold(KP k) { C::passC_fold(k); }
 
 
 // Node ramps of the mask table: f_j = (t_j + 1)/2 at the Chebyshev points
@@ -2716,6 +2875,20 @@ static bool fast_source(const PssPipeline &p) {
     return p.src == PSS_SRC_SEARCH && !p.gen_amp && p.gen_df == 1.0f && !p.inj_gen && p.null_mode != PSS_NULL_UNDELAYED &&
            p.nint <= kFastNint && !p.prof_split && (uint32_t)p.nint == p.knot_m;
 }
+// Fold-mode fast passes of the mixed-radix split (PairCols::passA_fold /
+// passC_fold): the fold source with chi2(df != 1) pair draws, and an
+// epilogue of noise only (any df != 1), no injected draws.
+static bool fold_source(const PssPipeline &p) {
+    if (g_flags & PSS_FLAG_NO_FAST) return false;
+    return p.src == PSS_SRC_FOLD && !p.gen_amp && !p.inj_gen && p.gen_df != 1.0f && p.nph > 0 &&
+           p.null_mode != PSS_NULL_UNDELAYED;
+}
+static bool fold_epilogue(const KP &k) {
+    const PssPipeline &p = k.p;
+    if (g_flags & PSS_FLAG_NO_FAST) return false;
+    if (p.out_kind != PSS_OUT_NONE || p.inj_noise || p.inj_rep) return false;
+    return p.noise && p.noise_df != 1.0f && p.null_mode != PSS_NULL_DELAYED;
+}
 static bool fast_epilogue(const KP &k) {
     const PssPipeline &p = k.p;
     if (g_flags & PSS_FLAG_NO_FAST) return false;
@@ -2973,7 +3146,15 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     using PR = PairRows<N2, TR, RF, RI>;
     dim3 gc((unsigned)(N2 / B), (unsigned)k.npairs);
     tk_begin(TK_COLA, st);
-    if constexpr (PC::kItemsExact) {
+    bool launched = false;
+    if constexpr (PC::kRegCols) {
+        if (fold_source(k.p)) {
+            k_pairA_fold<PC, T><<<gc, dim3(T), 0, st>>>(k);
+            launched = true;
+        }
+    }
+    if (launched) {
+    } else if constexpr (PC::kItemsExact) {
         if (fast_source(k.p)) {
             if (k.p.prof_rows == 1) k_pairA_fast<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
             else k_pairA_fast<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
@@ -3008,6 +3189,14 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
                 k_pairC_fast<PCC, TC, 2><<<dim3((unsigned)(N2 / BC / 2), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
             else
                 k_pairC_fast<PCC, TC, 1><<<dim3((unsigned)(N2 / BC), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
+        }
+    } else if (PC::kRegCols && fold_epilogue(k)) {
+        if constexpr (PC::kRegCols) {
+            // 128 columns per workgroup: the lane-private LDS staging of the
+            // column (N1 x 8 B per lane) then allows ~5 workgroups per CU
+            constexpr int FB = B > 128 ? 128 : B;
+            using PCF = PairCols<N1, FB, FB, CF, CI>;
+            k_pairC_fold<PCF, FB><<<dim3((unsigned)(N2 / FB), (unsigned)k.npairs), dim3(FB), 0, st>>>(k);
         }
     } else {
         k_pairC<PC, T><<<gc, dim3(T), 0, st>>>(k);

@@ -112,6 +112,50 @@ def test_fast_path_bitwise_equals_generic(nchan, log2n, null, dm, hip_lib):
     np.testing.assert_array_equal(fast, generic)
 
 
+F0_B1855 = 186.4940812499314404
+
+
+@pytest.mark.parametrize("nchan,shard,tobs,samprate_bins", [
+    (4, None, 1800.0, 1024),          # C4's geometry: 30 x 1024 (register columns, 30-point DFT)
+    (5, (1, 4), 1800.0, 1024),        # odd shard start: pair (0, 1) misses channel 0
+    (3, None, 600.0, 1024),           # 10 subints: 10 x 1024
+    (2, None, 720.0, 2048),           # 12 subints of 2048 bins: 24 x 1024
+])
+def test_fold_fast_bitwise_equals_generic(nchan, shard, tobs, samprate_bins, hip_lib):
+    """Fold mode on the mixed-radix split: the fold fast kernels
+    (k_pairA_fold / k_pairC_fold: chi2(Nfold) pair draws split over the
+    lanes of a column pair, one DPP swap) against the generic kernels
+    (source4 / epilogue4 draws through LDS), bit for bit; the generic path is
+    itself checked against the oracle with injected draws
+    (test_gpu_parity.py::test_c4_fold_mixed_radix_vs_oracle)."""
+    from psrsigsim_amd import _lib
+
+    def run():
+        import psrsigsim_amd as pss
+        from psrsigsim_amd.signal import FilterBankSignal
+        from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+        from psrsigsim_amd.ism import ISM
+        from psrsigsim_amd.telescope import telescope as T
+        pss.seed(29)
+        sig = FilterBankSignal(1400, 400, Nsubband=nchan, sample_rate=F0_B1855 * samprate_bins * 1e-6,
+                               sublen=60.0, fold=True, shard=shard)
+        psr = Pulsar(1.0 / F0_B1855, 0.005, profiles=GaussProfile(0.5, 0.05, 1))
+        psr.make_pulses(sig, tobs=tobs)
+        ISM().disperse(sig, 13.299393)
+        T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True)
+        return sig.data.cpu().numpy()
+
+    L = _lib.lib()
+    fast = run()
+    assert np.isfinite(fast).all()
+    old = L.pss_set_flags(_lib.FLAG_NO_FAST)
+    try:
+        generic = run()
+    finally:
+        L.pss_set_flags(old)
+    np.testing.assert_array_equal(fast, generic)
+
+
 def test_shard_invariance_odd_boundary_close(hip_lib):
     """Odd boundary: bit-for-bit only up to the pair partner's rounding."""
     full = _c3_small(8, None, 16)
