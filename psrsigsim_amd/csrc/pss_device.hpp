@@ -166,8 +166,26 @@ __device__ __forceinline__ float frac23(uint32_t x) {
 }
 
 // Four chi2(1) draws from one Philox block: z^2 with z Box-Muller normals,
-// -2 ln(u) cos^2(2 pi v) and -2 ln(u) sin^2(2 pi v).
+// -2 ln(u) cos^2(2 pi v) and -2 ln(u) sin^2(2 pi v), written as
+// h (1 + cos 4 pi v) and h (1 - cos 4 pi v), h = -ln u: one transcendental
+// per pair instead of two (the step is issue-bound and power-throttled).  The
+// angle 2v mod 1 is the top 23 bits below bit 31 of the word (4 pi v mod 2 pi
+// is uniform when v is).  Where the cosine is within an ulp of -1 or 1 the
+// small member of the pair is resolved to ~ulp(h) = h 6e-8 absolute
+// (chi2 values below ~1e-6; the distribution gates, tests/test_gpu_stats.py,
+// cover the sampler).
+#ifndef PSS_BM_ONE_TRIG
+#define PSS_BM_ONE_TRIG 1
+#endif
 __device__ __forceinline__ float4 chi2_1x4(uint4 r) {
+#if PSS_BM_ONE_TRIG
+    const float h0 = -0.6931471805599453f * __builtin_amdgcn_logf(u01(r.x));   // -ln u = -ln2 log2 u
+    const float h1 = -0.6931471805599453f * __builtin_amdgcn_logf(u01(r.z));
+    const float c0 = __builtin_amdgcn_cosf(frac23(r.y << 1));                 // cos(2 pi (2v mod 1))
+    const float c1 = __builtin_amdgcn_cosf(frac23(r.w << 1));
+    const float t0 = h0 * c0, t1 = h1 * c1;
+    return make_float4(h0 + t0, h0 - t0, h1 + t1, h1 - t1);
+#else
     float l0 = -1.3862943611198906f * __builtin_amdgcn_logf(u01(r.x));   // -2 ln u = -2 ln2 log2 u
     float l1 = -1.3862943611198906f * __builtin_amdgcn_logf(u01(r.z));
     float v0 = frac23(r.y);                                              // [0,1) revolutions
@@ -175,6 +193,7 @@ __device__ __forceinline__ float4 chi2_1x4(uint4 r) {
     float c0 = __builtin_amdgcn_cosf(v0), s0 = __builtin_amdgcn_sinf(v0);
     float c1 = __builtin_amdgcn_cosf(v1), s1 = __builtin_amdgcn_sinf(v1);
     return make_float4(l0 * c0 * c0, l0 * s0 * s0, l1 * c1 * c1, l1 * s1 * s1);
+#endif
 }
 
 // Four N(0, 1) draws from one Philox block (Box-Muller pairs

@@ -512,21 +512,33 @@ __global__ __launch_bounds__(256) void k_null_fix_list(KP k) {
         }
         if (__ballot(hits != 0u) == 0ull) continue;
         // (group, 4-bit mask) entries of this lane: samples n0 + j in groups
-        // of 4 aligned DATA indices (the Philox block of sample n is n >> 2)
-        const uint64_t below = (1ull << lane) - 1ull;
-        uint32_t total = 0;
+        // of 4 aligned DATA indices (the Philox block of sample n is n >> 2).
+        // Entries are listed lane-major (a lane's groups consecutive), so the
+        // lanes of the drawing loop below store consecutive 16-B groups of
+        // one word -- whole 128-B lines -- instead of one group of each of 64
+        // words per store instruction.  The exclusive prefix of the per-lane
+        // group counts (< 16) comes from four ballots.
         const uint32_t a = n0 & 3u;                      // offset of n0 in its group
         const uint64_t hx = (uint64_t)hits << a;         // hit bits by position in the aligned span
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int g = 0; g < 9; ++g) cnt += ((uint32_t)(hx >> (4 * g)) & 15u) ? 1u : 0u;
+        const uint64_t below = (1ull << lane) - 1ull;
+        uint32_t e = 0, total = 0;
+#pragma unroll
+        for (int bit = 0; bit < 4; ++bit) {
+            const uint64_t bal = __ballot((cnt >> bit) & 1u);
+            e += (uint32_t)__popcll(bal & below) << bit;
+            total += (uint32_t)__popcll(bal) << bit;
+        }
 #pragma unroll
         for (int g = 0; g < 9; ++g) {
             const uint32_t h = (uint32_t)(hx >> (4 * g)) & 15u;
-            const uint64_t bal = __ballot(h != 0u);
             if (h) {
-                const uint32_t e = total + (uint32_t)__popcll(bal & below);
                 desc[wv][e] = h;
                 dbase[wv][e] = ((n0 - a) + 4u * (uint32_t)g) & nm;   // first sample of the group
+                ++e;
             }
-            total += (uint32_t)__popcll(bal);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();

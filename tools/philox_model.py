@@ -10,7 +10,7 @@ can be studied on the CPU at sample sizes no GPU test would use:
 
   tools/philox_model.py study     -> profiles/r03/philox_quality.txt
 
-compares R = 7 and R = 10 on (a) KS p-values of the on-pulse selection of
+compares R = 7 (both Box-Muller forms) and R = 10 on (a) KS p-values of the on-pulse selection of
 tests/test_gpu_stats.py::test_search_pulse_draws_are_chi2_1 over 400 seeds
 (their distribution must be uniform), (b) lag correlations over 6.7e7
 draws, (c) mean / second moment over 6.7e7 draws."""
@@ -35,14 +35,24 @@ def philox(c0, c1, c2, c3, k0, k1, rounds):
     return c0, c1, c2, c3
 
 
-def chi2_1(n, chan, seed, call, purpose, rounds=7):
-    """Draws n = 0 .. n-1 of global channel `chan` (float64 arithmetic on the
-    device's 32-bit inputs: the model's values differ from the fp32 device
-    values only by rounding)."""
+def chi2_1(n, chan, seed, call, purpose, rounds=7, form="cos2"):
+    """Draws n = 0 .. n-1 of global channel `chan`.  form "cos2" (the device
+    default, PSS_BM_ONE_TRIG=1): h (1 +- cos 4 pi v), h = -ln u, with the
+    fp32 roundings of the device's last three operations (so the cancellation
+    of the small member of a pair is modelled); "two-trig": the previous
+    -2 ln u cos^2 / sin^2 form, float64."""
     blocks = np.arange((n + 3) // 4, dtype=np.uint64)
     r = philox(blocks, 0, chan, (call << 4) | purpose, seed & 0xFFFFFFFF, seed >> 32, rounds)
     u01 = lambda x: x.astype(np.float64) * 2.0 ** -32 + 2.0 ** -33
     fr = lambda x: (x >> np.uint64(9)).astype(np.float64) * 2.0 ** -23
+    if form == "cos2":
+        f32 = np.float32
+        fr2 = lambda x: ((x << np.uint64(1)) & MASK).astype(np.uint64)
+        h0, h1 = f32(-np.log(u01(r[0]))), f32(-np.log(u01(r[2])))
+        c0, c1 = f32(np.cos(2 * np.pi * fr(fr2(r[1])))), f32(np.cos(2 * np.pi * fr(fr2(r[3]))))
+        t0, t1 = h0 * c0, h1 * c1
+        out = np.stack([h0 + t0, h0 - t0, h1 + t1, h1 - t1], 1).astype(np.float64)
+        return out.ravel()[:n]
     l0, l1 = -2 * np.log(u01(r[0])), -2 * np.log(u01(r[2]))
     v0, v1 = 2 * np.pi * fr(r[1]), 2 * np.pi * fr(r[3])
     out = np.stack([l0 * np.cos(v0) ** 2, l0 * np.sin(v0) ** 2, l1 * np.cos(v1) ** 2, l1 * np.sin(v1) ** 2], 1)
@@ -61,20 +71,25 @@ def study(out):
     spp = (sig._samprate_MHz() * 0.005) * 1e6
     sel = psr.Profiles.calc_profiles((np.arange(n) / spp) % 1)[0] > 0.5
     lines = []
-    for R in (7, 10):
-        ps = np.array([stats.kstest(chi2_1(n, 0, s, 1, 1, R)[sel], stats.chi2(1).cdf).pvalue for s in range(1, 401)])
+    for R, form in ((7, "cos2"), (7, "two-trig"), (10, "two-trig")):
+        ps = np.array([stats.kstest(chi2_1(n, 0, s, 1, 1, R, form)[sel], stats.chi2(1).cdf).pvalue
+                       for s in range(1, 401)])
         lag = {}
         m1 = m2 = 0.0
+        small = 0
         for ch in range(8):
-            x = chi2_1(1 << 23, 10 + ch, 4242, 1, 1, R)
+            x = chi2_1(1 << 23, 10 + ch, 4242, 1, 1, R, form)
+            small += int((x < 1e-4).sum())
             m1 += x.mean() / 8
             m2 += (x * x).mean() / 8
             x = x - 1.0
             for l in (1, 2, 3, 4, 5, 8):
                 lag[l] = lag.get(l, 0.0) + np.mean(x[:-l] * x[l:]) / 2.0 / 8
         se = 1.0 / np.sqrt(8 * (1 << 23))
-        lines.append("Philox4x32-%d: on-pulse KS over 400 seeds: frac p<0.01 %.4f, p<0.05 %.4f, uniformity of the "
-                     "p-values (KS) %.3f" % (R, (ps < .01).mean(), (ps < .05).mean(), stats.kstest(ps, "uniform").pvalue))
+        lines.append("Philox4x32-%d, %s sampler: on-pulse KS over 400 seeds: frac p<0.01 %.4f, p<0.05 %.4f, "
+                     "uniformity of the p-values (KS) %.3f; P(x < 1e-4) = %.3e (chi2(1): %.3e)"
+                     % (R, form, (ps < .01).mean(), (ps < .05).mean(), stats.kstest(ps, "uniform").pvalue,
+                        small / (8.0 * (1 << 23)), stats.chi2(1).cdf(1e-4)))
         lines.append("  6.7e7 draws: mean-1 %.2e (SE %.1e), E[x^2]/3-1 %.2e (SE %.1e); lag correlations in SE units %s"
                      % (m1 - 1, np.sqrt(2 / 6.7e7), m2 / 3 - 1, np.sqrt(96 / 6.7e7) / 3,
                         {l: round(v / se, 2) for l, v in lag.items()}))
