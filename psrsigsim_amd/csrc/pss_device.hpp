@@ -177,10 +177,14 @@ __device__ __forceinline__ float frac23(uint32_t x) {
 #ifndef PSS_BM_ONE_TRIG
 #define PSS_BM_ONE_TRIG 1
 #endif
-__device__ __forceinline__ float4 chi2_1x4(uint4 r) {
+// `scale` multiplies the draws inside the sampler (h scale = (-ln2 scale)
+// log2 u: the product with the pulse draw_norm costs no extra instruction);
+// scale = 1 gives the plain chi2(1) values.
+__device__ __forceinline__ float4 chi2_1x4(uint4 r, float scale = 1.0f) {
 #if PSS_BM_ONE_TRIG
-    const float h0 = -0.6931471805599453f * __builtin_amdgcn_logf(u01(r.x));   // -ln u = -ln2 log2 u
-    const float h1 = -0.6931471805599453f * __builtin_amdgcn_logf(u01(r.z));
+    const float kl = -0.6931471805599453f * scale;
+    const float h0 = kl * __builtin_amdgcn_logf(u01(r.x));   // -ln u = -ln2 log2 u
+    const float h1 = kl * __builtin_amdgcn_logf(u01(r.z));
     const float c0 = __builtin_amdgcn_cosf(frac23(r.y << 1));                 // cos(2 pi (2v mod 1))
     const float c1 = __builtin_amdgcn_cosf(frac23(r.w << 1));
     const float t0 = h0 * c0, t1 = h1 * c1;
@@ -192,7 +196,7 @@ __device__ __forceinline__ float4 chi2_1x4(uint4 r) {
     float v1 = frac23(r.w);
     float c0 = __builtin_amdgcn_cosf(v0), s0 = __builtin_amdgcn_sinf(v0);
     float c1 = __builtin_amdgcn_cosf(v1), s1 = __builtin_amdgcn_sinf(v1);
-    return make_float4(l0 * c0 * c0, l0 * s0 * s0, l1 * c1 * c1, l1 * s1 * s1);
+    return make_float4(l0 * c0 * c0 * scale, l0 * s0 * s0 * scale, l1 * c1 * c1 * scale, l1 * s1 * s1 * scale);
 #endif
 }
 

@@ -671,29 +671,34 @@ __device__ __forceinline__ void pchip_locate(const KP &k, int64_t n, uint32_t &i
 }
 
 // The same (interval, fraction) for consecutive samples by increments: the
-// 96-bit product A(n) = (n phase_step mod 2^64) * knot_m, kept as (lo, u64 =
-// A >> 32), advances by D = phase_step * knot_m; when the phase wraps the
-// interval field comes back by knot_m.  Exact integer arithmetic: bitwise
-// the values pchip_locate computes, at three adds per sample instead of four
-// 32 x 32 -> 64 multiplies.
+// 96-bit product A(n) = (n phase_step mod 2^64) * knot_m, kept as three
+// 32-bit words (hi = interval field, mid = fraction, lo = guard), advances by
+// D = phase_step * knot_m; when the phase wraps the interval field comes back
+// by knot_m.  Exact integer arithmetic: bitwise the values pchip_locate
+// computes, at one add-with-carry chain and a min per sample (the 64-bit form
+// compiled to nine VALU per step) instead of four 32 x 32 -> 64 multiplies.
 struct PhaseWalk {
-    uint32_t lo;
-    uint64_t u64;
+    uint32_t lo, mid, hi;
     __device__ __forceinline__ void start(const PssPipeline &p, uint32_t n) {
         const uint64_t ph = (uint64_t)n * (uint32_t)p.phase_step + ((uint64_t)(n * (uint32_t)(p.phase_step >> 32)) << 32);
         const uint64_t t = (uint64_t)(uint32_t)ph * p.knot_m;
         lo = (uint32_t)t;
-        u64 = (uint64_t)(uint32_t)(ph >> 32) * p.knot_m + (t >> 32);
+        const uint64_t u64 = (uint64_t)(uint32_t)(ph >> 32) * p.knot_m + (t >> 32);
+        mid = (uint32_t)u64;
+        hi = (uint32_t)(u64 >> 32);
     }
     __device__ __forceinline__ void step(uint32_t dlo, uint64_t dhi, uint32_t M) {
-        const uint32_t l2 = lo + dlo;
-        u64 += dhi + (uint64_t)(l2 < lo);
-        lo = l2;
-        if ((uint32_t)(u64 >> 32) >= M) u64 -= (uint64_t)M << 32;
+        unsigned c;
+        lo = __builtin_addc(lo, dlo, 0u, &c);
+        mid = __builtin_addc(mid, (uint32_t)dhi, c, &c);
+        hi = hi + (uint32_t)(dhi >> 32) + c;
+        // (hi >= M) ? hi - M : hi -- hi < 2 M here, and for hi < M the
+        // difference wraps above hi (M <= 2^31)
+        hi = min(hi, hi - M);
     }
     __device__ __forceinline__ void get(const PssPipeline &p, uint32_t &iv, float &u) const {
-        iv = (uint32_t)(u64 >> 32);
-        u = frac23((uint32_t)u64);
+        iv = hi;
+        u = frac23(mid);
         if (iv >= (uint32_t)p.nint) {
             u += (float)(iv - (uint32_t)(p.nint - 1));
             iv = p.nint - 1;
@@ -703,8 +708,8 @@ struct PhaseWalk {
     // host's extrapolated pieces appended: pulsar._device_table), where
     // iv < knot_m needs no clamp -- bitwise what get() returns then
     __device__ __forceinline__ void get_full(uint32_t &iv, float &u) const {
-        iv = (uint32_t)(u64 >> 32);
-        u = frac23((uint32_t)u64);
+        iv = hi;
+        u = frac23(mid);
     }
 };
 __device__ __forceinline__ void phase_delta(const PssPipeline &p, uint32_t &dlo, uint64_t &dhi) {
@@ -770,6 +775,7 @@ __device__ __forceinline__ void source4(const KP &k, int r, int64_t n0, int cnt,
             for (int i = 0; i < 4; ++i) if (i < cnt) re[i] = row[n0 + i];
         } else {
             float x[4];
+            float dn = p.draw_norm;
             if (p.inj_gen) {
                 const float *row = p.inj_gen + (int64_t)r * k.N;
 #pragma unroll
@@ -778,6 +784,13 @@ __device__ __forceinline__ void source4(const KP &k, int r, int64_t n0, int cnt,
                 Rng g(p.seed, p.call_gen, P_PULSE);
                 const float4 z = normal_x4(g.bits((uint32_t)(n0 >> 2), c, (uint32_t)(n0 >> 34)));
                 x[0] = z.x; x[1] = z.y; x[2] = z.z; x[3] = z.w;
+            } else if (p.gen_df == 1.0f) {
+                // chi2(1) draws with draw_norm folded into the sampler (as the
+                // fast pass A draws them: bitwise the same values)
+                Rng g(p.seed, p.call_gen, P_PULSE);
+                const float4 q = chi2_1x4(g.bits((uint32_t)(n0 >> 2), c, (uint32_t)(n0 >> 34)), p.draw_norm);
+                x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
+                dn = 1.0f;                                   // (x * 1 is exact)
             } else {
                 Rng g(p.seed, p.call_gen, P_PULSE);
                 draw4(g, n0, c, p.gen_df, x);
@@ -789,19 +802,19 @@ __device__ __forceinline__ void source4(const KP &k, int r, int64_t n0, int cnt,
                 for (int i = 0; i < 4; ++i) {
                     if (i < cnt) {
                         const float pr = (p.gen_amp == 2) ? gauss_eval(k, n0 + i) : pchip_eval(k, prow, n0 + i);
-                        re[i] = sqrtf(fmaxf(pr, 0.0f)) * x[i] * p.draw_norm;
+                        re[i] = sqrtf(fmaxf(pr, 0.0f)) * x[i] * dn;
                     }
                 }
             } else if (p.src == PSS_SRC_SEARCH) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    if (i < cnt) re[i] = pchip_eval(k, prow, n0 + i) * x[i] * p.draw_norm;
+                    if (i < cnt) re[i] = pchip_eval(k, prow, n0 + i) * x[i] * dn;
             } else {   // FOLD
                 const float *pr = p.prof + (int64_t)prow * p.nph;
                 uint32_t b = (uint32_t)(n0 % p.nph);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    if (i < cnt) re[i] = pr[b] * x[i] * p.draw_norm;
+                    if (i < cnt) re[i] = pr[b] * x[i] * dn;
                     if (++b == (uint32_t)p.nph) b = 0;
                 }
             }
@@ -1508,6 +1521,10 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     // (consecutive lanes = consecutive columns: coalesced rows)
     static constexpr bool kRegCols = (B == T) && ((N1 & (N1 - 1)) != 0);
     static constexpr int kFoldWaves = N1 <= 30 ? 4 : 2;      // min waves per SIMD of the fold kernels
+    // passC_fold's lane-private LDS (N1 x 8 B per lane) caps its waves per
+    // SIMD at (160 KB / (N1 x 8 B x B)) x B / 256
+    static constexpr int kFoldWavesC = (160 * 1024 / (N1 * 8 * B)) * B / 256 < 1 ? 1
+                                     : ((160 * 1024 / (N1 * 8 * B)) * B / 256 > 4 ? 4 : (160 * 1024 / (N1 * 8 * B)) * B / 256);
     static_assert(B % 4 == 0, "4-sample items");
 
     // A: generate channels a, b into z = d_a + i d_b; column FFTs; twiddle; spill.
@@ -1573,8 +1590,9 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                     b4 = (it - n1 * (B / 4)) * 4;
                 }
                 const uint32_t n = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4;   // N <= 2^24
-                const float4 qa = chi2_1x4(g.bits(n >> 2, ca, 0u));
-                const float4 qb = chi2_1x4(g.bits(n >> 2, cb, 0u));
+                // draws scaled by draw_norm (0 for a pair's missing channel) in the sampler
+                const float4 qa = chi2_1x4(g.bits(n >> 2, ca, 0u), dna);
+                const float4 qb = chi2_1x4(g.bits(n >> 2, cb, 0u), dnb);
                 const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
 #if PSS_PHASE_WALK
                 PhaseWalk w;
@@ -1597,7 +1615,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                         const float4 Bc = ptab[1][iv];
                         pb = fmaf(fmaf(fmaf(Bc.x, u, Bc.y), u, Bc.z), u, Bc.w);
                     }
-                    lds[LdsC::at(b4 + i, n1)] = make_float2(pa * va[i] * dna, pb * vb[i] * dnb);
+                    lds[LdsC::at(b4 + i, n1)] = make_float2(pa * va[i], pb * vb[i]);
                 }
             }
         } else
@@ -2161,7 +2179,7 @@ __global__ __launch_bounds__(T) void k_node_col(KP k, float *nodes) { C::node_co
 template <typename C, int T>
 __global__ __launch_bounds__(T, C::kFoldWaves) void k_pairA_fold(KP k) { C::passA_fold(k); }
 template <typename C, int T>
-__global__ __launch_bounds__(T, C::kFoldWaves) void k_pairC_fold(KP k) { C::passC_fold(k); }
+__global__ __launch_bounds__(T, C::kFoldWavesC) void k_pairC_fold(KP k) { C::passC_fold(k); }
 
 
 // Node ramps of the mask table: f_j = (t_j + 1)/2 at the Chebyshev points
