@@ -1532,7 +1532,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     // injected draws, no undelayed null -- the same values as source4.
     template <bool FAST, bool SHARED = false>
     __device__ static void passA(const KP &k) {
-        __shared__ cf lds[B * LdsC::RS];
+        __shared__ __align__(128) cf lds[B * LdsC::RS];   // (128-B aligned: the FFT's byte-address exchanges)
         __shared__ cf tw16[kTw16Size];
         const int tid = threadIdx.x;
         tw16_fill(tw16, tid, T);     // read after the generate loop's barrier
@@ -1748,8 +1748,18 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             return;
         }
         for (int it = tid; it < N1 * B / 4; it += T) {
-            const int k1 = it / (B / 4);
-            const int b4 = (it - k1 * (B / 4)) * 4;
+            int k1, b4;
+            if constexpr (B < 32 && N1 % 32 == 0) {
+                // 32-lane groups: 32 consecutive rows of one 4-column group
+                // (the lanes of a store instruction still cover whole row
+                // segments, two lanes 32 apart per 64-B segment)
+                const int g = it >> 5;
+                b4 = (g % (B / 4)) * 4;
+                k1 = (g / (B / 4)) * 32 + (it & 31);
+            } else {
+                k1 = it / (B / 4);
+                b4 = (it - k1 * (B / 4)) * 4;
+            }
             cf a0 = lds[LdsC::at(b4 + 0, k1)], a1 = lds[LdsC::at(b4 + 1, k1)];
             cf a2 = lds[LdsC::at(b4 + 2, k1)], a3 = lds[LdsC::at(b4 + 3, k1)];
             PSS_DASSERT((int64_t)k1 * RP + n20 + b4 + 4 <= pstride(k));
@@ -1981,7 +1991,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     // C: inverse column FFTs of the data pair, then the epilogues of channels
     // a, b straight from LDS (delayed-null decisions from the mask table).
     __device__ static void passC(const KP &k) {
-        __shared__ cf lds[B * LdsC::RS];
+        __shared__ __align__(128) cf lds[B * LdsC::RS];   // (128-B aligned: the FFT's byte-address exchanges)
         const int tid = threadIdx.x;
         int cbx, pr;
         xcd_block(cbx, pr);
@@ -2036,7 +2046,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     template <int NBLK = 1>
     __device__ static void passC_fast(const KP &k) {
         static_assert(kItemsExact, "fast pass C: whole items per thread");
-        __shared__ __align__(16) cf lds[B * LdsC::RS];
+        __shared__ __align__(128) cf lds[B * LdsC::RS];
         const int tid = threadIdx.x;
         int cbx2, pr;
         xcd_block(cbx2, pr);
@@ -2139,7 +2149,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     // Mask table build: inverse column FFTs of node pair `blockIdx.y`, stored
     // (scaled) as node rows nodes[2 pr], nodes[2 pr + 1].
     __device__ static void node_col(const KP &k, float *nodes) {
-        __shared__ cf lds[B * LdsC::RS];
+        __shared__ __align__(128) cf lds[B * LdsC::RS];   // (128-B aligned: the FFT's byte-address exchanges)
         const int tid = threadIdx.x;
         int cbx, pr;
         xcd_block(cbx, pr);
@@ -3012,7 +3022,12 @@ static int build_mask_table(KP &k, hipStream_t st, const float *mask_row, char *
 // spill-store loop reads 4 columns x 16 rows per 32-lane group (a 32/B pitch
 // offset spreads the columns over the 64 read banks); pass C's load loop
 // writes 4 columns x 4 rows per 16-lane group (16/B over the 32 write banks).
-constexpr int xrs_read(int B) { return B >= 32 ? 1 : 32 / B; }
+// B < 32: a pitch that is a multiple of 16 complex, so the wave-local column
+// FFTs get the byte-address exchanges (Fft::XB: round 2's 4-complex pad cost
+// ~100 address VALU per lane in pass A); the spill-store loop then reads 32
+// consecutive rows of one 4-column group per 32-lane group (conflict-free at
+// any pitch, passA).
+constexpr int xrs_read(int B) { return B >= 32 ? 1 : 16; }
 // (pass C measured 0.5 ms faster on the padded layout at C3: its transposes
 // gain nothing from the swizzle and the XOR addressing costs VALU)
 constexpr int xrs_write(int B) { return -1; }
