@@ -58,6 +58,14 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 #ifndef PSS_WAVE_COLS
 #define PSS_WAVE_COLS 1
 #endif
+// fast pass C with 32-column blocks held in registers between LDS phases
+// (passC_fast32; the C3 1024 x 4096 split only); experiment switch.  Measured
+// (profiles/r03/s11, same box): pass C 16.86-16.89 ms against 16.75-16.81 --
+// the two register-held columns push the 1024-thread kernel to the 128-VGPR
+// cap and 20 VGPRs spill around the FFTs; bitwise equal (146 GPU tests)
+#ifndef PSS_PC32
+#define PSS_PC32 0
+#endif
 // fast pass C: column blocks per workgroup (2: the two halves of each 128-B
 // output line stored by the same lane back to back; 1: one block); experiment switch
 #ifndef PSS_PC_NBLK
@@ -2043,6 +2051,118 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     // channel row) leave the same lane in back-to-back stores instead of from
     // two workgroups (whose halves do not always meet in L2: PMC writes were
     // 1.11x the algorithmic bytes with NBLK = 1).
+    // C, fast path with 32-column blocks (PSS_PC32; N1 = 1024, T = 1024):
+    // 128-B output segments per channel row instead of 64 (tools/seg_bw.hip:
+    // 64-B write segments run at 5.2 TB/s against 6.6 for 128 B).  32 columns
+    // of 1024 rows are 256 KB, so they cannot all sit in LDS: each wave keeps
+    // its two columns (w, w + 16) in registers between three LDS phases --
+    // (1) the spill rows in two halves of 512 (256-B row segments, twiddled as
+    // in inv_block) staged in LDS and picked up into the FFT input mapping,
+    // (2) the two wave-local inverse FFTs one after the other through the
+    // wave's own LDS row, (3) each channel's scaled outputs staged as
+    // [n1][33] floats and stored as whole 128-B row segments with the noise.
+    // Bitwise the values of passC_fast (same twiddles, FFT and epilogue).
+    __device__ static void passC_fast32(const KP &k) {
+        static_assert(N1 == 1024 && B == 32 && T == 1024 && kWaveCols == false, "C3 split only");
+        constexpr int H = N1 / 2;                       // rows per load half
+        constexpr int RSH = H + H / 16 + 1;             // padded pitch of a half column (odd)
+        constexpr int OSP = B + 1;                      // staging pitch (floats)
+        using LW = Lds<N1, -1>;                         // FFT rows: padded, as passC_fast's
+        using FWC = Fft<N1, 1, 64, true, -1>;
+        constexpr int BUF = (B * RSH * 8 > 16 * LW::RS * 8 ? B * RSH * 8 : 16 * LW::RS * 8) > N1 * OSP * 4
+                                ? (B * RSH * 8 > 16 * LW::RS * 8 ? B * RSH * 8 : 16 * LW::RS * 8)
+                                : N1 * OSP * 4;
+        __shared__ __align__(16) char smem[BUF];
+        __shared__ cf tw16[kTw16Size];
+        const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+        tw16_fill(tw16, tid, T);
+        int cbx, pr;
+        xcd_block(cbx, pr);
+        const int ra = 2 * pr - k.poff, rb = ra + 1;
+        const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
+        const int64_t N2 = k.N2;
+        const PssPipeline &p = k.p;
+        const float invN = k.invN, nn = p.noise_norm;
+        const int64_t n20 = (int64_t)cbx * B;
+        const Buf Y(k.Yd + (int64_t)pr * pstride(k), (uint32_t)(pstride(k) * 8));
+        const uint32_t RP = (uint32_t)rpitch(k);
+        cf *hb = reinterpret_cast<cf *>(smem);
+        cf vA[16], vB[16];
+        // (1) spill rows, two halves
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (h) __syncthreads();                     // the first half has been picked up
+#pragma unroll 1
+            for (int it = tid; it < H * B / 4; it += T) {
+                const int k1l = it / (B / 4), b4 = (it - k1l * (B / 4)) * 4;
+                const int k1 = h * H + k1l;
+                const uint32_t off = ((uint32_t)k1 * RP + (uint32_t)b4) * 8u, so = (uint32_t)n20 * 8u;
+                const float4 lo = Y.ld4(off, so), hi = Y.ld4(off + 16u, so);
+                const cf a[4] = {make_float2(lo.x, lo.y), make_float2(lo.z, lo.w),
+                                 make_float2(hi.x, hi.y), make_float2(hi.z, hi.w)};
+                // the twiddles of inv_block, bit for bit
+                const uint32_t m0 = (uint32_t)(n20 + b4) * (uint32_t)k1;
+                float r0 = (float)m0 * invN;
+                if (r0 >= 0.5f) r0 -= 1.0f;
+                float r1 = (float)k1 * invN;
+                if (r1 >= 0.5f) r1 -= 1.0f;
+                const cf w0 = expi_rev(r0), w1 = expi_rev(r1);
+                const cf w2 = cmul(w1, w1);
+                const cf tw[4] = {w0, cmul(w0, w1), cmul(w0, w2), cmul(w0, cmul(w2, w1))};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) hb[(b4 + i) * RSH + k1l + (k1l >> 4)] = cmul(a[i], tw[i]);
+            }
+            __syncthreads();
+            // the FFT input mapping of radix 16 over 1024: lane holds positions lane + 64 q
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int pl = lane + 64 * q;
+                vA[8 * h + q] = hb[wv * RSH + pl + (pl >> 4)];
+                vB[8 * h + q] = hb[(wv + 16) * RSH + pl + (pl >> 4)];
+            }
+        }
+        __syncthreads();
+        // (2) the two inverse column FFTs through the wave's own LDS row
+        {
+            cf *wl = reinterpret_cast<cf *>(smem) + wv * LW::RS;
+            if constexpr (!(kAbl & 2)) FWC::template run_tw<true, 1, I...>(vA, wl, lane, tw16);
+            stage_sync<true>();
+            if constexpr (!(kAbl & 2)) FWC::template run_tw<true, 1, I...>(vB, wl, lane, tw16);
+        }
+        // (3) per channel: stage the scaled outputs, store rows with the noise
+        constexpr int RIL = FWC::template last_of<I...>();
+        float *stg = reinterpret_cast<float *>(smem);
+        const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
+        const Rng gn(p.seed, p.call_noise, P_NOISE);
+        const uint32_t rbytes = (uint32_t)(k.N * 4);
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch) {
+            __syncthreads();                            // FFT rows / previous channel's staging free
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                int bb, pos;
+                FWC::template where<RIL>(i, lane, bb, pos);
+                stg[pos * OSP + wv] = (ch ? vA[i].y : vA[i].x) * invN;
+                stg[pos * OSP + wv + 16] = (ch ? vB[i].y : vB[i].x) * invN;
+            }
+            __syncthreads();
+            const bool has = ch ? hasb : hasa;
+            if (!has) continue;                         // (uniform)
+            const uint32_t c = ch ? cb : ca;
+            const Buf o(p.data + (int64_t)(ch ? rb : ra) * p.ld, rbytes);
+#pragma unroll
+            for (int t = 0; t < N1 * B / 4 / T; ++t) {
+                const int it = tid + t * T;
+                const int n1 = it / (B / 4), c4 = (it - n1 * (B / 4)) * 4;
+                const uint32_t n = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)c4;
+                const float4 x = chi2_1x4(gn.bits(n >> 2, c, 0u));
+                const float *sr = stg + n1 * OSP + c4;
+                o.st4(fmaf(nn, x.x, sr[0]), fmaf(nn, x.y, sr[1]), fmaf(nn, x.z, sr[2]), fmaf(nn, x.w, sr[3]),
+                      n * 4u, 0);
+            }
+        }
+    }
+
     template <int NBLK = 1>
     __device__ static void passC_fast(const KP &k) {
         static_assert(kItemsExact, "fast pass C: whole items per thread");
@@ -2182,6 +2302,8 @@ template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairC(KP k) { C::passC(k); }
 template <typename C, int T, int NBLK>
 __global__ __launch_bounds__(T) void k_pairC_fast(KP k) { C::template passC_fast<NBLK>(k); }
+template <typename C, int T>
+__global__ __launch_bounds__(T) void k_pairC_fast32(KP k) { C::passC_fast32(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_node_col(KP k, float *nodes) { C::node_col(k, nodes); }
 // (4 waves per SIMD for columns up to 30: the compiler would otherwise keep
@@ -3230,7 +3352,10 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
             // PSS_PC_NBLK = 2: two adjacent column blocks per workgroup
             // (rejected from the ISA, not run: block 0's 32 output registers stay live
             // through block 1 and the kernel spills 31 VGPRs at the 128 cap)
-            if constexpr (PSS_PC_NBLK == 2 && (N2 / BC) % 2 == 0)
+            if constexpr (PSS_PC32 && N1 == 1024 && N2 % 32 == 0 && TC == 1024)
+                k_pairC_fast32<PairCols<N1, 32, 1024, CF, CI, -1>, 1024>
+                    <<<dim3((unsigned)(N2 / 32), (unsigned)k.npairs), dim3(1024), 0, st>>>(k);
+            else if constexpr (PSS_PC_NBLK == 2 && (N2 / BC) % 2 == 0)
                 k_pairC_fast<PCC, TC, 2><<<dim3((unsigned)(N2 / BC / 2), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
             else
                 k_pairC_fast<PCC, TC, 1><<<dim3((unsigned)(N2 / BC), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
