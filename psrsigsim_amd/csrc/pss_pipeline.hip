@@ -1362,6 +1362,11 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
             // pair ramp factors (k_pair_tab): {E, D} per q, wave-uniform
             const cf *ptab = k.rtab + (int64_t)pr * (2 * RFL);
             const uint64_t hsum = (rwa >> 1) + (rwb >> 1), hdif = (rwa >> 1) - (rwb >> 1);
+            // RFL = 16 (the C3 4096-point rows): the bins of a butterfly as one
+            // straight-line body under a scalar branch (the form below measured
+            // neutral at C3 and 0.8 ms slower on C5's 8192-point rows, RFL = 8,
+            // profiles/r03/s6: those keep the per-bin form)
+            if constexpr (RFL == 16) {
 #pragma unroll
             for (int ib = 0; ib < E / RFL; ++ib) {
                 const int jg = tid + ib * T;
@@ -1442,6 +1447,71 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                         bin(q, lds[LD::at(bm, k2m)]);
                     }
                 }
+            }
+            } else {
+#pragma unroll
+            for (int ib = 0; ib < E / RFL; ++ib) {
+                const int jg = tid + ib * T, b = jg / LRL, jj = jg - b * LRL;
+                const int row = b ? rowB : rowA;
+                const int64_t kb0 = row + (int64_t)N1 * jj;
+                const cf bE = expi_rev(-fix_to_rev((uint64_t)kb0 * hsum));
+                const cf bD = expi_rev(-fix_to_rev((uint64_t)kb0 * hdif));
+                // mirror bins k2m = N2 - 1 - k2 = P0 - q LRL (all but row 0 of
+                // the {0, N1/2} pair, whose bin 0 pairs with itself): with
+                // LRL % 256 == 0 the swizzle XOR is the same for every q, so
+                // the reads are one byte base minus immediate offsets
+                constexpr bool kMirXB = FF::XB && (LRL % 256 == 0);
+                const bool affine = !(j == 0 && row == 0);       // wave-uniform
+                uint32_t mbase = 0;
+                if constexpr (kMirXB) mbase = lds_byte(lds) + 8u * (uint32_t)LD::at(j == 0 ? b : 1 - b, N2 - 1 - jj);
+#pragma unroll
+                for (int q = 0; q < RFL; ++q) {
+                    const int i = ib * RFL + q, k2 = jj + q * LRL;
+                    cf Zm;
+                    if (kMirXB && affine) {
+                        Zm = lds_ld(mbase - 8u * (uint32_t)(q * LRL));
+                    } else {
+                        int bm, k2m;
+                        if (j == 0) { bm = b; k2m = (row == 0) ? ((N2 - k2) & (N2 - 1)) : (N2 - 1 - k2); }
+                        else        { bm = 1 - b; k2m = N2 - 1 - k2; }
+                        Zm = lds[LD::at(bm, k2m)];
+                    }
+                    const cf Z = v[i];
+                    // 2 D_a and 2 D_b (DC / Nyquist and the tail extension)
+                    const cf Sa = make_float2(Z.x + Zm.x, Z.y - Zm.y);
+                    const cf Sb = make_float2(Z.y + Zm.y, Zm.x - Z.x);
+                    if constexpr (kAbl & 8) {
+                        v[i] = cadd(Sa, Sb);
+                    } else if (kb0 == 0 && 2 * q == RFL) {          // Nyquist bin
+                        float fa = k.p.nyq_re[ra], fb = k.p.nyq_re[rb];
+                        if constexpr (TAIL) {                       // H(N/2) = (1-a)/(1+a)
+                            const float ta = k.p.tail_a[ra], tb = k.p.tail_a[rb];
+                            fa *= (1.0f - ta) / (1.0f + ta);
+                            fb *= (1.0f - tb) / (1.0f + tb);
+                        }
+                        v[i] = make_float2((0.5f * Sa.x) * fa, (0.5f * Sb.x) * fb);
+                    } else if (kb0 == 0 && q == 0) {                // DC (H = 1)
+                        const cf Da = make_float2(0.5f * Sa.x, 0.5f * Sa.y), Db = make_float2(0.5f * Sb.x, 0.5f * Sb.y);
+                        v[i] = make_float2(Da.x - Db.y, Da.y + Db.x);
+                    } else {
+                        const cf Ef = cmul(bE, ptab[2 * q]), Df = cmul(bD, ptab[2 * q + 1]);
+                        if constexpr (TAIL) {
+                            // per-channel transfer functions: R_a = E D, R_b = E conj(D)
+                            const cf w = bin_phasor(kb0 + (int64_t)q * (k.N / RFL), k.N);
+                            const cf ra_ = cmul(make_float2(0.5f * Ef.x, 0.5f * Ef.y), cmul(Df, tail_factor(k.p.tail_a[ra], w)));
+                            const cf rb_ = cmul(make_float2(0.5f * Ef.x, 0.5f * Ef.y), cmul_conj(tail_factor(k.p.tail_a[rb], w), Df));
+                            const cf A = cmul(Sa, ra_);
+                            const cf Bv = cmul(Sb, rb_);
+                            v[i] = make_float2(A.x - Bv.y, A.y + Bv.x);
+                        } else {
+                            // W = E (Z cos d - i conj(Zm) sin d), D = cos d - i sin d
+                            const float c = Df.x, s = -Df.y;
+                            const cf in = make_float2(fmaf(Z.x, c, -(Zm.y * s)), fmaf(Z.y, c, -(Zm.x * s)));
+                            v[i] = cmul(Ef, in);
+                        }
+                    }
+                }
+            }
             }
             __syncthreads();
             if constexpr (!(kAbl & 2)) FF::template run_tw_c<true, kTwc, 1, I...>(v, lds, tid, tw16, twc);
