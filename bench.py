@@ -61,13 +61,16 @@ TOBS_PER_SAMPLE = 20.48e-6
 # value (pair mode), i.e. 4 B per channel-sample per spill pass; the null mask
 # is a once-per-run table (no per-channel bytes).
 #   colA: write spill 4 | row: read 4 + write 4 | colC: read spill 4 + write fp32 4
-#   null_fix: rewrite the nulled samples, 4 B each.  C3's null(0.1) picks
-#   round(0.1 nsub) whole periods, but the reference thresholds the FFT-shifted
-#   chi2(100) box mask at > 1 (pulsar.py:306-330), and the boxes' Gibbs ringing
-#   crosses that threshold around every nulled period too: ~16 % of each
-#   channel's samples end up nulled (PMC, profiles/r02: 5.57 GB of writes per
-#   launch = 0.65 B/ch-sample), so that measured fraction is what is booked
-NULL_FRAC_C3 = 0.16
+#   null_fix: rewrite the nulled samples, 4 B each.  C3's null(0.1) nulls
+#   round(0.1 nsub) whole periods, and the reference thresholds the FFT-shifted
+#   chi2(100) box mask at > 1 (pulsar.py:306-330), whose Gibbs ringing crosses
+#   the threshold next to the boxes too: 10.1-10.9 % of a channel's samples
+#   end up nulled (the oracle's shifted mask at C3's parameters, 8 channels
+#   across the band, two seeds; DESIGN.md "Roofline accounting").  PMC writes
+#   of the fix-up: 3.91 GB per launch = 0.455 B per channel-sample, 1.08x the
+#   4 x 0.105 booked here (profiles/r03/pmc_traffic.json; round 2's 5.5 GB
+#   was partial-line write amplification, removed by the lane-major entries)
+NULL_FRAC_C3 = 0.105
 ALG_BYTES = {"fourstep_colA": 4.0, "fourstep_row": 8.0, "fourstep_colC": 8.0, "null_fix": 4.0 * NULL_FRAC_C3,
              "single_pass": 4.0, "elementwise": 8.0, "fallback_dft": 28.0}
 

@@ -58,6 +58,14 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 #ifndef PSS_WAVE_COLS
 #define PSS_WAVE_COLS 1
 #endif
+// row pass of the 1024 x 4096 split with 1024 threads (8 values each, radix
+// 8^4) for 8 waves per SIMD instead of 4 (experiment switch).  Measured
+// (profiles/r03/s12, same box): row 21.2-21.3 ms against 15.3-15.4 -- at the
+// 64-VGPR budget of 8 waves the kernel spills 12 VGPRs, and the fourth
+// radix-8 stage adds an LDS exchange
+#ifndef PSS_ROW8
+#define PSS_ROW8 0
+#endif
 // fast pass C with 32-column blocks held in registers between LDS phases
 // (passC_fast32; the C3 1024 x 4096 split only); experiment switch.  Measured
 // (profiles/r03/s11, same box): pass C 16.86-16.89 ms against 16.75-16.81 --
@@ -1309,6 +1317,10 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
     static_assert(RIL == RF0, "inverse plan must be the reversed forward plan");
     static constexpr int LR = N2 / RF0;
     static constexpr int LRL = N2 / RFL;
+    // minimum waves per SIMD the kernel is compiled for (VGPR budget 512 /
+    // waves): two workgroups per CU when two rows fit twice in LDS; the
+    // 1024-thread 4096-point variant (PSS_ROW8) aims at 8
+    static constexpr int kMinWaves = (T <= 512) ? 2 * T / 256 : (N2 <= 4096 ? 8 : 4);
     // byte offset of (row, n2) in a pair spill (PSS_PAIR_IL: side b of row
     // pair p), and the offset step of the q-th first-stage input (n2 + q LR)
     static constexpr uint32_t kQS = (kPairIL ? 16u : 8u) * (uint32_t)LR;
@@ -1563,7 +1575,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
 };
 
 template <typename R, int T, bool TAIL = false>
-__global__ __launch_bounds__(T, (T <= 512 ? 2 * T / 256 : 4)) void k_pair_row(KP k) { R::template pass<false, TAIL>(k); }
+__global__ __launch_bounds__(T, R::kMinWaves) void k_pair_row(KP k) { R::template pass<false, TAIL>(k); }
 template <typename R, int T>
 __global__ __launch_bounds__(T) void k_node_row(KP k) { R::template pass<true>(k); }
 
@@ -2984,6 +2996,7 @@ using C1kI = RList<4, 16, 16>;
 using C2kF = RList<16, 16, 8>;
 using C2kI = RList<8, 16, 16>;
 using C4k = RList<16, 16, 16>;
+using C4k8 = RList<8, 8, 8, 8>;     // 4096 = 8^4: 8 values per thread at 1024 threads (PSS_ROW8)
 using C8kF = RList<16, 8, 8, 8>;
 using C8kI = RList<8, 8, 8, 16>;
 
@@ -3464,7 +3477,10 @@ static int run_fourstep(KP &k, hipStream_t st, const float *mask_row) {
     if (kSplit4k && N == (1 << 22)) {
         k.N2 = 4096;
         k.N1 = 1024;
-        return launch_pair<1024, 8, 512, C1kF, C1kF, 4096, 512, C4k, C4k, 256, PSS_BC, PSS_TC>(k, st, mask_row);
+        if constexpr (PSS_ROW8)
+            return launch_pair<1024, 8, 512, C1kF, C1kF, 4096, 1024, C4k8, C4k8, 256, PSS_BC, PSS_TC>(k, st, mask_row);
+        else
+            return launch_pair<1024, 8, 512, C1kF, C1kF, 4096, 512, C4k, C4k, 256, PSS_BC, PSS_TC>(k, st, mask_row);
     }
     if (N == (1 << 22)) {
         // 512 x 8192 split (layout experiment; the 1024 x 4096 split above is
