@@ -70,9 +70,15 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 // (passC_fast32; the C3 1024 x 4096 split only); experiment switch.  Measured
 // (profiles/r03/s11, same box): pass C 16.86-16.89 ms against 16.75-16.81 --
 // the two register-held columns push the 1024-thread kernel to the 128-VGPR
-// cap and 20 VGPRs spill around the FFTs; bitwise equal (146 GPU tests)
+// cap and 20 VGPRs spill around the FFTs; bitwise equal (146 GPU tests).  The
+// 512-thread form (4 columns per wave, 235 VGPRs, no spill, 2 waves per
+// SIMD): 16.80-16.83 against 16.44-16.50 (profiles/r03/s13) -- the wider
+// output segments do not pay for the extra phases at this occupancy
 #ifndef PSS_PC32
 #define PSS_PC32 0
+#endif
+#ifndef PSS_PC32_T     // its threads: 1024 (2 columns per wave) or 512 (4 per wave, 256 VGPRs)
+#define PSS_PC32_T 512
 #endif
 // fast pass C: column blocks per workgroup (2: the two halves of each 128-B
 // output line stored by the same lane back to back; 1: one block); experiment switch
@@ -2145,7 +2151,8 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     // [n1][33] floats and stored as whole 128-B row segments with the noise.
     // Bitwise the values of passC_fast (same twiddles, FFT and epilogue).
     __device__ static void passC_fast32(const KP &k) {
-        static_assert(N1 == 1024 && B == 32 && T == 1024 && kWaveCols == false, "C3 split only");
+        static_assert(N1 == 1024 && B == 32 && (T == 1024 || T == 512) && kWaveCols == false, "C3 split only");
+        constexpr int NW = T / 64, CPW = B / NW;        // waves, columns per wave
         constexpr int H = N1 / 2;                       // rows per load half
         constexpr int RSH = H + H / 16 + 1;             // padded pitch of a half column (odd)
         constexpr int OSP = B + 1;                      // staging pitch (floats)
@@ -2169,7 +2176,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         const Buf Y(k.Yd + (int64_t)pr * pstride(k), (uint32_t)(pstride(k) * 8));
         const uint32_t RP = (uint32_t)rpitch(k);
         cf *hb = reinterpret_cast<cf *>(smem);
-        cf vA[16], vB[16];
+        cf v[CPW][16];
         // (1) spill rows, two halves
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -2199,17 +2206,19 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const int pl = lane + 64 * q;
-                vA[8 * h + q] = hb[wv * RSH + pl + (pl >> 4)];
-                vB[8 * h + q] = hb[(wv + 16) * RSH + pl + (pl >> 4)];
+#pragma unroll
+                for (int c = 0; c < CPW; ++c) v[c][8 * h + q] = hb[(wv + NW * c) * RSH + pl + (pl >> 4)];
             }
         }
         __syncthreads();
         // (2) the two inverse column FFTs through the wave's own LDS row
         {
             cf *wl = reinterpret_cast<cf *>(smem) + wv * LW::RS;
-            if constexpr (!(kAbl & 2)) FWC::template run_tw<true, 1, I...>(vA, wl, lane, tw16);
-            stage_sync<true>();
-            if constexpr (!(kAbl & 2)) FWC::template run_tw<true, 1, I...>(vB, wl, lane, tw16);
+#pragma unroll
+            for (int c = 0; c < CPW; ++c) {
+                if (c) stage_sync<true>();
+                if constexpr (!(kAbl & 2)) FWC::template run_tw<true, 1, I...>(v[c], wl, lane, tw16);
+            }
         }
         // (3) per channel: stage the scaled outputs, store rows with the noise
         constexpr int RIL = FWC::template last_of<I...>();
@@ -2224,8 +2233,8 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             for (int i = 0; i < 16; ++i) {
                 int bb, pos;
                 FWC::template where<RIL>(i, lane, bb, pos);
-                stg[pos * OSP + wv] = (ch ? vA[i].y : vA[i].x) * invN;
-                stg[pos * OSP + wv + 16] = (ch ? vB[i].y : vB[i].x) * invN;
+#pragma unroll
+                for (int c = 0; c < CPW; ++c) stg[pos * OSP + wv + NW * c] = (ch ? v[c][i].y : v[c][i].x) * invN;
             }
             __syncthreads();
             const bool has = ch ? hasb : hasa;
@@ -2385,7 +2394,7 @@ __global__ __launch_bounds__(T) void k_pairC(KP k) { C::passC(k); }
 template <typename C, int T, int NBLK>
 __global__ __launch_bounds__(T) void k_pairC_fast(KP k) { C::template passC_fast<NBLK>(k); }
 template <typename C, int T>
-__global__ __launch_bounds__(T) void k_pairC_fast32(KP k) { C::passC_fast32(k); }
+__global__ __launch_bounds__(T, T == 512 ? 2 : 4) void k_pairC_fast32(KP k) { C::passC_fast32(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_node_col(KP k, float *nodes) { C::node_col(k, nodes); }
 // (4 waves per SIMD for columns up to 30: the compiler would otherwise keep
@@ -3436,8 +3445,8 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
             // (rejected from the ISA, not run: block 0's 32 output registers stay live
             // through block 1 and the kernel spills 31 VGPRs at the 128 cap)
             if constexpr (PSS_PC32 && N1 == 1024 && N2 % 32 == 0 && TC == 1024)
-                k_pairC_fast32<PairCols<N1, 32, 1024, CF, CI, -1>, 1024>
-                    <<<dim3((unsigned)(N2 / 32), (unsigned)k.npairs), dim3(1024), 0, st>>>(k);
+                k_pairC_fast32<PairCols<N1, 32, PSS_PC32_T, CF, CI, -1>, PSS_PC32_T>
+                    <<<dim3((unsigned)(N2 / 32), (unsigned)k.npairs), dim3(PSS_PC32_T), 0, st>>>(k);
             else if constexpr (PSS_PC_NBLK == 2 && (N2 / BC) % 2 == 0)
                 k_pairC_fast<PCC, TC, 2><<<dim3((unsigned)(N2 / BC / 2), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
             else
