@@ -58,6 +58,11 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 #ifndef PSS_WAVE_COLS
 #define PSS_WAVE_COLS 1
 #endif
+// C5's 2048 x 8192 split: pass C too with one wave per 8-column block's
+// column (512 threads; experiment switch, measured slower)
+#ifndef PSS_C5_WAVE
+#define PSS_C5_WAVE 0
+#endif
 // row pass of the 1024 x 4096 split with 1024 threads (8 values each, radix
 // 8^4) for 8 waves per SIMD instead of 4 (experiment switch).  Measured
 // (profiles/r03/s12, same box): row 21.2-21.3 ms against 15.3-15.4 -- at the
@@ -3503,7 +3508,15 @@ static int run_fourstep(KP &k, hipStream_t st, const float *mask_row) {
         // (1024 threads, 139 KB LDS) for 32-B output segments instead of 16
         k.N2 = 8192;
         k.N1 = 2048;
-        return launch_pair<2048, 4, 512, C2kF, C2kF, 8192, 1024, C8kF, C8kI, 512, 8, 1024>(k, st, mask_row);
+        // pass A: 8 columns, one wave per 2048-point column (wave-local FFTs,
+        // 32 values per lane; 64-B spill segments): 40.5 -> 33.3 ms against
+        // the 4-column workgroup-FFT kernel (profiles/r03/s14, one box).  The
+        // same for pass C (PSS_C5_WAVE) measured 44.5-44.9 -> 47.8-48.0: pass
+        // C keeps 1024 threads on its 8 columns.
+        if constexpr (PSS_C5_WAVE)
+            return launch_pair<2048, 8, 512, C2kF, C2kF, 8192, 1024, C8kF, C8kI, 512, 8, 512>(k, st, mask_row);
+        else
+            return launch_pair<2048, 8, 512, C2kF, C2kF, 8192, 1024, C8kF, C8kI, 512, 8, 1024>(k, st, mask_row);
     }
     if (PSS_ROW4K && N >= (1 << 17) && N <= (1 << 21)) {
         // rows of 4096 (the C3 row kernel: two rows of a pair in 66 KB, two
