@@ -63,6 +63,11 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 #ifndef PSS_C5_WAVE
 #define PSS_C5_WAVE 0
 #endif
+// C5: pass C with 16-column blocks (64-B output segments instead of 32) held in
+// registers between LDS phases, 2 columns per wave (passC_fast32)
+#ifndef PSS_C5_WIDE
+#define PSS_C5_WIDE 1
+#endif
 // row pass of the 1024 x 4096 split with 1024 threads (8 values each, radix
 // 8^4) for 8 waves per SIMD instead of 4 (experiment switch).  Measured
 // (profiles/r03/s12, same box): row 21.2-21.3 ms against 15.3-15.4 -- at the
@@ -2156,16 +2161,19 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     // [n1][33] floats and stored as whole 128-B row segments with the noise.
     // Bitwise the values of passC_fast (same twiddles, FFT and epilogue).
     __device__ static void passC_fast32(const KP &k) {
-        static_assert(N1 == 1024 && B == 32 && (T == 1024 || T == 512) && kWaveCols == false, "C3 split only");
+        static_assert((N1 == 1024 || N1 == 2048) && (T == 1024 || T == 512) && B % (T / 64) == 0 &&
+                      kWaveCols == false, "register-resident wide pass C: 2^m columns of 1024 / 2048");
         constexpr int NW = T / 64, CPW = B / NW;        // waves, columns per wave
+        constexpr int E1 = N1 / 64;                     // values per lane of one column
         constexpr int H = N1 / 2;                       // rows per load half
         constexpr int RSH = H + H / 16 + 1;             // padded pitch of a half column (odd)
         constexpr int OSP = B + 1;                      // staging pitch (floats)
         using LW = Lds<N1, -1>;                         // FFT rows: padded, as passC_fast's
         using FWC = Fft<N1, 1, 64, true, -1>;
-        constexpr int BUF = (B * RSH * 8 > 16 * LW::RS * 8 ? B * RSH * 8 : 16 * LW::RS * 8) > N1 * OSP * 4
-                                ? (B * RSH * 8 > 16 * LW::RS * 8 ? B * RSH * 8 : 16 * LW::RS * 8)
-                                : N1 * OSP * 4;
+        constexpr int RI0 = FWC::template first<I...>();
+        constexpr int LRI = N1 / RI0;                   // input mapping: v[ib RI0 + q] = lane + 64 ib + LRI q
+        constexpr int B1 = B * RSH * 8, B2 = NW * LW::RS * 8, B3 = N1 * OSP * 4;
+        constexpr int BUF = (B1 > B2 ? B1 : B2) > B3 ? (B1 > B2 ? B1 : B2) : B3;
         __shared__ __align__(16) char smem[BUF];
         __shared__ cf tw16[kTw16Size];
         const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -2181,7 +2189,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         const Buf Y(k.Yd + (int64_t)pr * pstride(k), (uint32_t)(pstride(k) * 8));
         const uint32_t RP = (uint32_t)rpitch(k);
         cf *hb = reinterpret_cast<cf *>(smem);
-        cf v[CPW][16];
+        cf v[CPW][E1];
         // (1) spill rows, two halves
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -2207,16 +2215,19 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                 for (int i = 0; i < 4; ++i) hb[(b4 + i) * RSH + k1l + (k1l >> 4)] = cmul(a[i], tw[i]);
             }
             __syncthreads();
-            // the FFT input mapping of radix 16 over 1024: lane holds positions lane + 64 q
+            // the FFT input mapping: register i = ib RI0 + q holds position
+            // lane + 64 ib + LRI q (the half it lies in is compile-time)
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int pl = lane + 64 * q;
+            for (int i = 0; i < E1; ++i) {
+                const int pc = 64 * (i / RI0) + LRI * (i % RI0);      // position minus lane
+                if (pc / H != h) continue;
+                const int pl = lane + pc - h * H;
 #pragma unroll
-                for (int c = 0; c < CPW; ++c) v[c][8 * h + q] = hb[(wv + NW * c) * RSH + pl + (pl >> 4)];
+                for (int c = 0; c < CPW; ++c) v[c][i] = hb[(wv + NW * c) * RSH + pl + (pl >> 4)];
             }
         }
         __syncthreads();
-        // (2) the two inverse column FFTs through the wave's own LDS row
+        // (2) the inverse column FFTs through the wave's own LDS row
         {
             cf *wl = reinterpret_cast<cf *>(smem) + wv * LW::RS;
 #pragma unroll
@@ -2235,7 +2246,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         for (int ch = 0; ch < 2; ++ch) {
             __syncthreads();                            // FFT rows / previous channel's staging free
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
+            for (int i = 0; i < E1; ++i) {
                 int bb, pos;
                 FWC::template where<RIL>(i, lane, bb, pos);
 #pragma unroll
@@ -3449,7 +3460,10 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
             // PSS_PC_NBLK = 2: two adjacent column blocks per workgroup
             // (rejected from the ISA, not run: block 0's 32 output registers stay live
             // through block 1 and the kernel spills 31 VGPRs at the 128 cap)
-            if constexpr (PSS_PC32 && N1 == 1024 && N2 % 32 == 0 && TC == 1024)
+            if constexpr (PSS_C5_WIDE && N1 == 2048 && N2 % 16 == 0)
+                k_pairC_fast32<PairCols<N1, 16, 512, CF, CI, -1>, 512>
+                    <<<dim3((unsigned)(N2 / 16), (unsigned)k.npairs), dim3(512), 0, st>>>(k);
+            else if constexpr (PSS_PC32 && N1 == 1024 && N2 % 32 == 0 && TC == 1024)
                 k_pairC_fast32<PairCols<N1, 32, PSS_PC32_T, CF, CI, -1>, PSS_PC32_T>
                     <<<dim3((unsigned)(N2 / 32), (unsigned)k.npairs), dim3(PSS_PC32_T), 0, st>>>(k);
             else if constexpr (PSS_PC_NBLK == 2 && (N2 / BC) % 2 == 0)
