@@ -68,6 +68,11 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 #ifndef PSS_C5_WIDE
 #define PSS_C5_WIDE 1
 #endif
+// 8192-point data rows (C5) one row at a time through LDS, both in
+// registers, two workgroups per CU (PairRowsSeq)
+#ifndef PSS_ROW_SEQ
+#define PSS_ROW_SEQ 1
+#endif
 // row pass of the 1024 x 4096 split with 1024 threads (8 values each, radix
 // 8^4) for 8 waves per SIMD instead of 4 (experiment switch).  Measured
 // (profiles/r03/s12, same box): row 21.2-21.3 ms against 15.3-15.4 -- at the
@@ -1594,6 +1599,191 @@ template <typename R, int T, bool TAIL = false>
 __global__ __launch_bounds__(T, R::kMinWaves) void k_pair_row(KP k) { R::template pass<false, TAIL>(k); }
 template <typename R, int T>
 __global__ __launch_bounds__(T) void k_node_row(KP k) { R::template pass<true>(k); }
+
+// Row pass of a data pair with the two rows of a row pair in registers and
+// ONE row in LDS (PSS_ROW_SEQ; the 8192-point rows of C5's 2048 x 8192
+// split): PairRows holds both rows in LDS (2 x 65.7 KB, one workgroup per
+// CU, so every barrier stalls the CU); here each exchange moves one row
+// through a 65.7-KB buffer and two workgroups share a CU.  Same stages and
+// ramp arithmetic as PairRows::pass<false> (no tail extension).  After the
+// forward transforms a thread holds row A's bins k2 = jj + q LRL and reads
+// row B's at the mirrors N2-1-k2; it then forms W_A(k2) and W_B(N2-1-k2)
+// from the same pair of values, and W_B goes back to the thread mapping
+// through one more exchange.  Row pair {0, N1/2} (each row its own mirror,
+// DC and Nyquist in row 0) takes the per-row form.
+template <int N2, int T, typename FWD, typename INV>
+struct PairRowsSeq;
+
+// a value the compiler cannot see through (no CSE across uses)
+__device__ __forceinline__ int opaque(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+template <int N2, int T, int... F, int... I>
+struct PairRowsSeq<N2, T, RList<F...>, RList<I...>> {
+    using FF = Fft<N2, 1, T, false, 16>;
+    using LD = typename FF::LD;
+    using PRW = PairRows<N2, T, RList<F...>, RList<I...>>;   // spill addressing
+    static constexpr int E = FF::E;                           // values per thread of ONE row
+    static constexpr int RF0 = FF::template first<F...>();
+    static constexpr int RFL = FF::template last_of<F...>();
+    static constexpr int LR = N2 / RF0;
+    static constexpr int LRL = N2 / RFL;
+    static_assert(FF::template last_of<I...>() == RF0 && FF::template first<I...>() == RFL,
+                  "inverse plan must be the reversed forward plan");
+    static_assert(E / RF0 * T <= LR && E / RFL * T <= LRL, "one row per thread mapping");
+
+    // W = E (Z cos d - i conj(Zm) sin d) of bin kb0 + q N/RFL (PairRows::pass)
+    __device__ static __forceinline__ cf ramp(cf Z, cf Zm, cf bE, cf bD, const cf *ptab, int q) {
+        const cf Ef = cmul(bE, ptab[2 * q]), Df = cmul(bD, ptab[2 * q + 1]);
+        const float c = Df.x, s = -Df.y;
+        return cmul(Ef, make_float2(fmaf(Z.x, c, -(Zm.y * s)), fmaf(Z.y, c, -(Zm.x * s))));
+    }
+
+    // SELF: row pair {0, N1/2} (its own launch: a branch between the two
+    // forms makes the compiler spill both rows at the branch)
+    template <bool SELF>
+    __device__ static void pass(const KP &k) {
+        __shared__ __align__(128) cf lds[LD::RS];
+        __shared__ cf tw16[kTw16Size];
+        const int tid = threadIdx.x;
+        tw16_fill(tw16, tid, T);
+        const int pr = blockIdx.x;
+        const int j = SELF ? 0 : (int)blockIdx.y + 1;   // row pair {j, N1-j}; {0, N1/2}
+        const int N1 = (int)k.N1;
+        const int rowA = j, rowB = (j == 0) ? N1 / 2 : N1 - j;
+        const int ra = max(2 * pr - k.poff, 0), rb = min(2 * pr + 1 - k.poff, k.p.nchan - 1);
+        const uint64_t rwa = (uint64_t)k.p.ramp[ra], rwb = (uint64_t)k.p.ramp[rb];
+        const uint64_t hsum = (rwa >> 1) + (rwb >> 1), hdif = (rwa >> 1) - (rwb >> 1);
+        const cf *ptab = k.rtab + (int64_t)pr * (2 * RFL);
+        const uint32_t RP = (uint32_t)rpitch(k);
+        const Buf Y(k.Yd + (int64_t)pr * pstride(k), (uint32_t)(pstride(k) * 8));
+        cf va[E], vb[E];
+        // one row's registers live across the other's transform, not two
+        // rows' loads in flight (the 128-VGPR budget of 4 waves per SIMD)
+        auto load = [&](cf (&v)[E], int row, int b) __attribute__((always_inline)) {
+#pragma unroll
+            for (int ib = 0; ib < E / RF0; ++ib) {
+                const uint32_t o = PRW::spill_off(RP, j, row, b, tid + ib * T);
+#pragma unroll
+                for (int q = 0; q < RF0; ++q) v[ib * RF0 + q] = Y.ld2(o, q * PRW::kQS);
+            }
+        };
+        // (each transform ends with a barrier after its last LDS read, so
+        // the next one may scatter at once)
+        // opaque(tid) per transform: the four transforms have identical
+        // LDS address arithmetic, and without it the compiler keeps one
+        // set of addresses live across the kernel (spilled) instead of
+        // recomputing them
+        load(va, rowA, 0);
+        FF::template run_tw<false, 1, F...>(va, lds, opaque(tid), tw16);
+        load(vb, rowB, 1);
+        FF::template run_tw<false, 1, F...>(vb, lds, opaque(tid), tw16);
+        if constexpr (!SELF) {
+            // row B to LDS; row B at the mirrors of this thread's row-A bins
+            FF::template store<RFL>(vb, lds, opaque(tid));
+            __syncthreads();
+#pragma unroll
+            for (int ib = 0; ib < E / RFL; ++ib) {
+                const int jj = tid + ib * T;
+                const uint32_t mbase = lds_byte(lds) + 8u * (uint32_t)LD::at(0, N2 - 1 - jj);
+#pragma unroll
+                for (int q = 0; q < RFL; ++q) {
+                    if constexpr (FF::XB && LRL % 256 == 0) vb[ib * RFL + q] = lds_ld(mbase - 8u * (uint32_t)(q * LRL));
+                    else vb[ib * RFL + q] = lds[LD::at(0, N2 - 1 - jj - q * LRL)];
+                }
+            }
+#pragma unroll
+            for (int ib = 0; ib < E / RFL; ++ib) {
+                const int jj = tid + ib * T, jm = LRL - 1 - jj;
+                const int64_t ka = rowA + (int64_t)N1 * jj, kbm = rowB + (int64_t)N1 * jm;
+                const cf aE = expi_rev(-fix_to_rev((uint64_t)ka * hsum));
+                const cf aD = expi_rev(-fix_to_rev((uint64_t)ka * hdif));
+                const cf bE = expi_rev(-fix_to_rev((uint64_t)kbm * hsum));
+                const cf bD = expi_rev(-fix_to_rev((uint64_t)kbm * hdif));
+#pragma unroll
+                for (int q = 0; q < RFL; ++q) {
+                    const int i = ib * RFL + q;
+                    const cf Za = va[i], Zb = vb[i];      // A at k2, B at N2-1-k2
+                    va[i] = ramp(Za, Zb, aE, aD, ptab, q);
+                    vb[i] = ramp(Zb, Za, bE, bD, ptab, RFL - 1 - q);
+                }
+            }
+            // W_B from the mirror positions back to the thread mapping
+            __syncthreads();
+#pragma unroll
+            for (int ib = 0; ib < E / RFL; ++ib) {
+                const int jj = tid + ib * T;
+                const uint32_t mbase = lds_byte(lds) + 8u * (uint32_t)LD::at(0, N2 - 1 - jj);
+#pragma unroll
+                for (int q = 0; q < RFL; ++q) {
+                    if constexpr (FF::XB && LRL % 256 == 0) lds_st(mbase - 8u * (uint32_t)(q * LRL), vb[ib * RFL + q]);
+                    else lds[LD::at(0, N2 - 1 - jj - q * LRL)] = vb[ib * RFL + q];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int ib = 0; ib < E / RFL; ++ib) {
+                const int jj = tid + ib * T;
+#pragma unroll
+                for (int q = 0; q < RFL; ++q) vb[ib * RFL + q] = lds[LD::at(0, jj + q * LRL)];
+            }
+            __syncthreads();
+        } else {
+            // rows 0 and N1/2: each its own mirror (row 0: bin 0 with itself)
+            auto self = [&](cf (&v)[E], int row) __attribute__((always_inline)) {
+                FF::template store<RFL>(v, lds, opaque(tid));
+                __syncthreads();
+#pragma unroll
+                for (int ib = 0; ib < E / RFL; ++ib) {
+                    const int jj = tid + ib * T;
+                    const int64_t kb0 = row + (int64_t)N1 * jj;
+                    const cf bE = expi_rev(-fix_to_rev((uint64_t)kb0 * hsum));
+                    const cf bD = expi_rev(-fix_to_rev((uint64_t)kb0 * hdif));
+#pragma unroll
+                    for (int q = 0; q < RFL; ++q) {
+                        const int i = ib * RFL + q, k2 = jj + q * LRL;
+                        const int k2m = (row == 0) ? ((N2 - k2) & (N2 - 1)) : (N2 - 1 - k2);
+                        const cf Z = v[i], Zm = lds[LD::at(0, k2m)];
+                        const cf Sa = make_float2(Z.x + Zm.x, Z.y - Zm.y);
+                        const cf Sb = make_float2(Z.y + Zm.y, Zm.x - Z.x);
+                        if (kb0 == 0 && 2 * q == RFL) {          // Nyquist bin
+                            v[i] = make_float2((0.5f * Sa.x) * k.p.nyq_re[ra], (0.5f * Sb.x) * k.p.nyq_re[rb]);
+                        } else if (kb0 == 0 && q == 0) {         // DC (H = 1)
+                            const cf Da = make_float2(0.5f * Sa.x, 0.5f * Sa.y), Db = make_float2(0.5f * Sb.x, 0.5f * Sb.y);
+                            v[i] = make_float2(Da.x - Db.y, Da.y + Db.x);
+                        } else {
+                            v[i] = ramp(Z, Zm, bE, bD, ptab, q);
+                        }
+                    }
+                }
+                __syncthreads();
+            };
+            self(va, rowA);
+            self(vb, rowB);
+        }
+        FF::template run_tw<true, 1, I...>(va, lds, opaque(tid), tw16);
+#pragma unroll
+        for (int ib = 0; ib < E / RF0; ++ib) {
+            const int jj = tid + ib * T;
+            const uint32_t oa = PRW::spill_off(RP, j, rowA, 0, jj);
+#pragma unroll
+            for (int q = 0; q < RF0; ++q) Y.st2(va[ib * RF0 + q], oa, q * PRW::kQS);
+        }
+        FF::template run_tw<true, 1, I...>(vb, lds, opaque(tid), tw16);
+#pragma unroll
+        for (int ib = 0; ib < E / RF0; ++ib) {
+            const int jj = tid + ib * T;
+            const uint32_t ob = PRW::spill_off(RP, j, rowB, 1, jj);
+#pragma unroll
+            for (int q = 0; q < RF0; ++q) Y.st2(vb[ib * RF0 + q], ob, q * PRW::kQS);
+        }
+    }
+};
+
+template <typename R, int T, bool SELF>
+__global__ __launch_bounds__(T, SELF ? T / 256 : 2 * T / 256) void k_pair_row_seq(KP k) { R::template pass<SELF>(k); }
 
 
 // XRS: extra row pitch of the LDS column block (Lds), chosen per kernel for
@@ -3443,10 +3633,15 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     LAUNCHCHK();
     if (k.after_a && !g_batch_after_row) HIPCHK(hipEventRecord(k.after_a, st));   // batching: the next batch's pass A may start
     tk_begin(TK_ROW, st);
-    if (k.p.tail_a)
+    if (k.p.tail_a) {
         k_pair_row<PR, TR, true><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
-    else
+    } else if constexpr (PSS_ROW_SEQ && N2 == 8192) {
+        using PRS = PairRowsSeq<N2, 512, RF, RI>;
+        k_pair_row_seq<PRS, 512, false><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2 - 1)), dim3(512), 0, st>>>(k);
+        k_pair_row_seq<PRS, 512, true><<<dim3((unsigned)k.npairs, 1u), dim3(512), 0, st>>>(k);
+    } else {
         k_pair_row<PR, TR><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
+    }
     tk_end(st);
     LAUNCHCHK();
     if (k.after_a && g_batch_after_row) HIPCHK(hipEventRecord(k.after_a, st));
