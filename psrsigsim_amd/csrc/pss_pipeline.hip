@@ -73,6 +73,13 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 #ifndef PSS_ROW_SEQ
 #define PSS_ROW_SEQ 1
 #endif
+// the same for C3's 4096-point rows (256 threads, up to 4 workgroups per CU;
+// experiment switch).  Measured (profiles/r03/s18, same box): row 19.6-19.7
+// ms with radix 16^3 (36 VGPRs spilled), 17.4-17.5 ms with 8^4 (PSS_ROW8=1),
+// against 15.2-15.3 ms for both rows in LDS at two workgroups per CU
+#ifndef PSS_ROW_SEQ4K
+#define PSS_ROW_SEQ4K 0
+#endif
 // row pass of the 1024 x 4096 split with 1024 threads (8 values each, radix
 // 8^4) for 8 waves per SIMD instead of 4 (experiment switch).  Measured
 // (profiles/r03/s12, same box): row 21.2-21.3 ms against 15.3-15.4 -- at the
@@ -1783,7 +1790,7 @@ struct PairRowsSeq<N2, T, RList<F...>, RList<I...>> {
 };
 
 template <typename R, int T, bool SELF>
-__global__ __launch_bounds__(T, SELF ? T / 256 : 2 * T / 256) void k_pair_row_seq(KP k) { R::template pass<SELF>(k); }
+__global__ __launch_bounds__(T, SELF ? 1 : 4) void k_pair_row_seq(KP k) { R::template pass<SELF>(k); }
 
 
 // XRS: extra row pitch of the LDS column block (Lds), chosen per kernel for
@@ -3635,10 +3642,11 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     tk_begin(TK_ROW, st);
     if (k.p.tail_a) {
         k_pair_row<PR, TR, true><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
-    } else if constexpr (PSS_ROW_SEQ && N2 == 8192) {
-        using PRS = PairRowsSeq<N2, 512, RF, RI>;
-        k_pair_row_seq<PRS, 512, false><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2 - 1)), dim3(512), 0, st>>>(k);
-        k_pair_row_seq<PRS, 512, true><<<dim3((unsigned)k.npairs, 1u), dim3(512), 0, st>>>(k);
+    } else if constexpr (PSS_ROW_SEQ && (N2 == 8192 || (PSS_ROW_SEQ4K && N2 == 4096))) {
+        constexpr int TS = N2 / 16;                  // 16 values of each row per thread
+        using PRS = PairRowsSeq<N2, TS, RF, RI>;
+        k_pair_row_seq<PRS, TS, false><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2 - 1)), dim3(TS), 0, st>>>(k);
+        k_pair_row_seq<PRS, TS, true><<<dim3((unsigned)k.npairs, 1u), dim3(TS), 0, st>>>(k);
     } else {
         k_pair_row<PR, TR><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
     }
