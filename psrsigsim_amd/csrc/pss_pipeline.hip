@@ -74,9 +74,11 @@ static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
 #define PSS_ROW_SEQ 1
 #endif
 // the same for C3's 4096-point rows (256 threads, up to 4 workgroups per CU;
-// experiment switch).  Measured (profiles/r03/s18, same box): row 19.6-19.7
-// ms with radix 16^3 (36 VGPRs spilled), 17.4-17.5 ms with 8^4 (PSS_ROW8=1),
-// against 15.2-15.3 ms for both rows in LDS at two workgroups per CU
+// experiment switch).  Measured (profiles/r03/s18, s19, same box): row
+// 19.6-19.7 ms with radix 16^3 (36 VGPRs spilled), 17.4-17.5 ms with 8^4
+// (PSS_ROW8=1); with row B's thread relabelling (no mirror exchanges)
+// 16.8 / 17.0 ms -- against 15.3-15.5 ms for both rows in LDS at two
+// workgroups per CU
 #ifndef PSS_ROW_SEQ4K
 #define PSS_ROW_SEQ4K 0
 #endif
@@ -1613,11 +1615,11 @@ __global__ __launch_bounds__(T) void k_node_row(KP k) { R::template pass<true>(k
 // CU, so every barrier stalls the CU); here each exchange moves one row
 // through a 65.7-KB buffer and two workgroups share a CU.  Same stages and
 // ramp arithmetic as PairRows::pass<false> (no tail extension).  After the
-// forward transforms a thread holds row A's bins k2 = jj + q LRL and reads
-// row B's at the mirrors N2-1-k2; it then forms W_A(k2) and W_B(N2-1-k2)
-// from the same pair of values, and W_B goes back to the thread mapping
-// through one more exchange.  Row pair {0, N1/2} (each row its own mirror,
-// DC and Nyquist in row 0) takes the per-row form.
+// forward transforms a thread holds row A's bins k2 = jj + q LRL and row
+// B's at the mirrors N2-1-k2 (row B's thread relabelling below); it forms
+// W_A(k2) and W_B(N2-1-k2) from the same pair of registers.  Row pair {0,
+// N1/2} (each row its own mirror, DC and Nyquist in row 0) takes the
+// per-row form through LDS.
 template <int N2, int T, typename FWD, typename INV>
 struct PairRowsSeq;
 
@@ -1669,38 +1671,33 @@ struct PairRowsSeq<N2, T, RList<F...>, RList<I...>> {
         cf va[E], vb[E];
         // one row's registers live across the other's transform, not two
         // rows' loads in flight (the 128-VGPR budget of 4 waves per SIMD)
-        auto load = [&](cf (&v)[E], int row, int b) __attribute__((always_inline)) {
+        auto load = [&](cf (&v)[E], int row, int b, int t) __attribute__((always_inline)) {
 #pragma unroll
             for (int ib = 0; ib < E / RF0; ++ib) {
-                const uint32_t o = PRW::spill_off(RP, j, row, b, tid + ib * T);
+                const uint32_t o = PRW::spill_off(RP, j, row, b, t + ib * T);
 #pragma unroll
                 for (int q = 0; q < RF0; ++q) v[ib * RF0 + q] = Y.ld2(o, q * PRW::kQS);
             }
         };
+        // Row B runs as thread tb = T-1-tid (a relabelling of the threads:
+        // every stage and both spill accesses use tb).  With LRL = (E/RFL) T
+        // its last forward stage leaves, in register E-1-i, row B's bin
+        // N2-1-k2 -- the mirror of row A's bin k2 in register i -- so the
+        // ramp pairs registers without an LDS exchange, and W_B is already
+        // in thread tb's inverse input mapping.
+        const int tb = SELF ? tid : T - 1 - tid;
         // (each transform ends with a barrier after its last LDS read, so
         // the next one may scatter at once)
-        // opaque(tid) per transform: the four transforms have identical
+        // opaque(...) per transform: the four transforms have identical
         // LDS address arithmetic, and without it the compiler keeps one
         // set of addresses live across the kernel (spilled) instead of
         // recomputing them
-        load(va, rowA, 0);
+        load(va, rowA, 0, tid);
         FF::template run_tw<false, 1, F...>(va, lds, opaque(tid), tw16);
-        load(vb, rowB, 1);
-        FF::template run_tw<false, 1, F...>(vb, lds, opaque(tid), tw16);
+        load(vb, rowB, 1, tb);
+        FF::template run_tw<false, 1, F...>(vb, lds, opaque(tb), tw16);
         if constexpr (!SELF) {
-            // row B to LDS; row B at the mirrors of this thread's row-A bins
-            FF::template store<RFL>(vb, lds, opaque(tid));
-            __syncthreads();
-#pragma unroll
-            for (int ib = 0; ib < E / RFL; ++ib) {
-                const int jj = tid + ib * T;
-                const uint32_t mbase = lds_byte(lds) + 8u * (uint32_t)LD::at(0, N2 - 1 - jj);
-#pragma unroll
-                for (int q = 0; q < RFL; ++q) {
-                    if constexpr (FF::XB && LRL % 256 == 0) vb[ib * RFL + q] = lds_ld(mbase - 8u * (uint32_t)(q * LRL));
-                    else vb[ib * RFL + q] = lds[LD::at(0, N2 - 1 - jj - q * LRL)];
-                }
-            }
+            static_assert(E / RFL * T == LRL, "mirror registers need LRL = (E/RFL) T");
 #pragma unroll
             for (int ib = 0; ib < E / RFL; ++ib) {
                 const int jj = tid + ib * T, jm = LRL - 1 - jj;
@@ -1712,31 +1709,11 @@ struct PairRowsSeq<N2, T, RList<F...>, RList<I...>> {
 #pragma unroll
                 for (int q = 0; q < RFL; ++q) {
                     const int i = ib * RFL + q;
-                    const cf Za = va[i], Zb = vb[i];      // A at k2, B at N2-1-k2
+                    const cf Za = va[i], Zb = vb[E - 1 - i];      // A at k2, B at N2-1-k2
                     va[i] = ramp(Za, Zb, aE, aD, ptab, q);
-                    vb[i] = ramp(Zb, Za, bE, bD, ptab, RFL - 1 - q);
+                    vb[E - 1 - i] = ramp(Zb, Za, bE, bD, ptab, RFL - 1 - q);
                 }
             }
-            // W_B from the mirror positions back to the thread mapping
-            __syncthreads();
-#pragma unroll
-            for (int ib = 0; ib < E / RFL; ++ib) {
-                const int jj = tid + ib * T;
-                const uint32_t mbase = lds_byte(lds) + 8u * (uint32_t)LD::at(0, N2 - 1 - jj);
-#pragma unroll
-                for (int q = 0; q < RFL; ++q) {
-                    if constexpr (FF::XB && LRL % 256 == 0) lds_st(mbase - 8u * (uint32_t)(q * LRL), vb[ib * RFL + q]);
-                    else lds[LD::at(0, N2 - 1 - jj - q * LRL)] = vb[ib * RFL + q];
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int ib = 0; ib < E / RFL; ++ib) {
-                const int jj = tid + ib * T;
-#pragma unroll
-                for (int q = 0; q < RFL; ++q) vb[ib * RFL + q] = lds[LD::at(0, jj + q * LRL)];
-            }
-            __syncthreads();
         } else {
             // rows 0 and N1/2: each its own mirror (row 0: bin 0 with itself)
             auto self = [&](cf (&v)[E], int row) __attribute__((always_inline)) {
@@ -1778,10 +1755,10 @@ struct PairRowsSeq<N2, T, RList<F...>, RList<I...>> {
 #pragma unroll
             for (int q = 0; q < RF0; ++q) Y.st2(va[ib * RF0 + q], oa, q * PRW::kQS);
         }
-        FF::template run_tw<true, 1, I...>(vb, lds, opaque(tid), tw16);
+        FF::template run_tw<true, 1, I...>(vb, lds, opaque(tb), tw16);
 #pragma unroll
         for (int ib = 0; ib < E / RF0; ++ib) {
-            const int jj = tid + ib * T;
+            const int jj = tb + ib * T;
             const uint32_t ob = PRW::spill_off(RP, j, rowB, 1, jj);
 #pragma unroll
             for (int q = 0; q < RF0; ++q) Y.st2(vb[ib * RF0 + q], ob, q * PRW::kQS);
