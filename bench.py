@@ -21,17 +21,20 @@ launcher (torchrun / torch.distributed.run: WORLD_SIZE set) every rank runs
 its channel block; invoked directly with --gpus N > 1, bench.py launches the
 N ranks itself (torch.distributed.run as a child process, before anything in
 this process touches the GPU) and exits with their status.
-  --scaling weak   (default): each rank owns its own 2048-channel block of a
-                   2048*N-channel signal (fixed work per GPU);
-  --scaling strong : the BASELINE C3 definition -- ONE 2048-channel signal
-                   split into N contiguous channel blocks (shard.channel_block).
+  --scaling strong (default for C3/C2/C4): the BASELINE C3 definition -- ONE
+                   2048-channel signal split into N contiguous channel blocks
+                   (shard.channel_block): 2048/N channels per rank;
+  --scaling weak   (default for C5, whose BASELINE config IS per GPU: 1024 of
+                   8192 channels each): every rank owns its own --nchan block.
 No collective on the data path (shard-invariant RNG keyed by global channel);
 the timing barrier and the max-over-ranks reduction are the only RCCL calls
 (the C4 workload adds the gather of the folded product).
 
 Reports (one JSON line on rank 0): value = channel-samples/s over all ranks,
 the roofline of the dominant kernel (HIP events on the launch stream, inside
-the timed region), and the CPU oracle timed on a bounded channel sample; next
+the timed region) and of the whole step (roofline.pipeline_frac: algorithmic
+bytes of every kernel of a step / ms_per_step / 8 TB/s), and the CPU oracle
+timed on a bounded channel sample; next
 to them the first and steady step spans (step_ms_first / step_ms_steady: the
 first timed step starts on an idle GPU and carries its host planning) and the
 GPU's socket power and gfx clock through the timed steps (gpu_power).
@@ -164,11 +167,12 @@ def c2_step(pss, nchan_total, shard, nsamp_log2, plan_group=None):
 
 
 WORKLOADS = {
-    "c2": "C2: NANOGrav L-band search mode 512 ch x 2^20 samp per GPU, J1713+0747 DataProfile (P=1/218.81 Hz), "
+    "c2": "C2: NANOGrav L-band search mode 512 ch x 2^20 samp, J1713+0747 DataProfile (P=1/218.81 Hz), "
           "disperse(DM=15.917131) + GBT Lband_GUPPI radiometer noise",
-    "c3": "C3 north-star: FilterBankSignal 2048 ch x 2^22 samp per GPU, GaussProfile P=5 ms, "
+    "c3": "C3 north-star: FilterBankSignal 2048 ch x 2^22 samp (strong: one signal channel-sharded over the "
+          "GPUs), GaussProfile P=5 ms, "
           "scatter_broaden(1e-4 s, convolve) + disperse(DM=100) + null(0.1) + Arecibo Lband_PUPPI radiometer noise",
-    "c4": "C4: fold mode 2048 ch x (30 subints x 1024 bins) per GPU, P=1/186.49 Hz, B1855+09 template "
+    "c4": "C4: fold mode 2048 ch x (30 subints x 1024 bins), P=1/186.49 Hz, B1855+09 template "
           "DataProfile, disperse(DM=13.3) + Arecibo noise, RCCL gather of the folded filterbank to rank 0",
     "c5": "C5 per GPU: 1024 ch x 2^24 samp (8192 ch over 8 GPUs), GaussProfile P=5 ms, disperse(DM=500) + "
           "Arecibo noise",
@@ -364,13 +368,15 @@ def launch_ranks(n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
-                    help="weak: --nchan channels per GPU; strong: --nchan channels in total, split over the GPUs")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default=None,
+                    help="strong (default; c5: weak): --nchan channels in total, split over the GPUs; "
+                         "weak: --nchan channels per GPU")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU-only check of the launcher / JSON contract: host planning only, gloo, no GPU")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--nchan", type=int, default=NCHAN, help="channels per GPU")
+    ap.add_argument("--nchan", type=int, default=NCHAN,
+                    help="channels in total (strong scaling) or per GPU (weak)")
     ap.add_argument("--log2n", type=int, default=LOG2N)
     ap.add_argument("--cpu-chans", type=int, default=32, help="oracle sample size (channels; BASELINE.md §3: 32)")
     ap.add_argument("--cpu-workers", type=int, default=16,
@@ -401,6 +407,8 @@ def main():
     if args.workload == "c4":
         args.log2n = None
         args.no_cpu = True
+    if args.scaling is None:
+        args.scaling = "weak" if args.workload == "c5" else "strong"
 
     import torch
     import torch.distributed as dist
@@ -552,13 +560,22 @@ def main():
         b = ALG_BYTES.get(k, 0.0) * full
         kernels[k] = {"avg_ms": round(avg, 4), "launches": n, "alg_bytes": b,
                       "GBps": round(b / (avg * 1e-3) / 1e9, 1)}
+    # the whole step against the HBM roofline: every kernel's algorithmic
+    # bytes of one step (all ranks) over the wall time per step
+    step_bytes = sum(ALG_BYTES.get(k, 0.0) * full * n for k, (ms, n) in agg.items()) / max(args.steps, 1) \
+        * (float(total) / C)
     if dom is not None:
         avg_ms = agg[dom][0] / agg[dom][1]
         bytes_launch = ALG_BYTES[dom] * full
         ach = bytes_launch / (avg_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
-                "avg_launch_ms": round(avg_ms, 4), "alg_bytes_per_launch": bytes_launch}
+                "avg_launch_ms": round(avg_ms, 4), "alg_bytes_per_launch": bytes_launch,
+                "pipeline_alg_bytes_per_step": step_bytes,
+                "pipeline_achieved": round(step_bytes / per_step / 1e9, 1),
+                "pipeline_frac": round(step_bytes / per_step / 1e9 / (HBM_PEAK_GBS * world), 4),
+                "pipeline_frac_basis": "all kernels' algorithmic bytes per step (ALG_BYTES x channel-samples) "
+                                       "/ ms_per_step / (8 TB/s x n_gpus)"}
         # measured HBM bytes per launch of this kernel (rocprofv3 PMC passes,
         # tools/pmc_round.sh + tools/pmc_traffic.py; C3 size only)
         for rnd in ("r03", "r02"):
@@ -584,8 +601,9 @@ def main():
                                                                                          args.log2n, dta)}
         cpu = {"value": round(v, 1), "unit": "channel-samples/s", "cores": 1, "kind": "port",
                "sample": "%d ch x 2^%d samp of the same C3 pipeline, oracle/pss_cpu.py (float64 NumPy, "
-                         "reference call structure), single process, %.1f s on %s"
-                         % (args.cpu_chans, args.log2n, dt, cpu_model())}
+                         "reference call structure; like the reference it also builds observe's pre-noise "
+                         "out copy, ~2%% of its time, which the GPU run elides when ret_resampsig=False), "
+                         "single process, %.1f s on %s" % (args.cpu_chans, args.log2n, dt, cpu_model())}
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "channel-samples/s",

@@ -149,6 +149,9 @@ class Pulsar(object):
         signal._ncols = int(signal._nsamp)
         signal._pending = _engine.Pending(src)
         signal._row0 = None
+        # new data: an earlier null()'s tie error / pending checks no longer apply
+        signal._null_error = None
+        signal._null_checks = []
 
     def _make_pow_pulses(self, signal):
         """pulsar.py:185-244: fold -> tile(profiles, nsub) x chi2(Nfold);
@@ -190,6 +193,9 @@ class Pulsar(object):
         signal._ncols = int(ncols)
         signal._pending = _engine.Pending(src)
         signal._row0 = None
+        # new data: an earlier null()'s tie error / pending checks no longer apply
+        signal._null_error = None
+        signal._null_checks = []
 
     def null(self, signal, null_frac, length=None, frequency=None):
         """pulsar.py:246-333."""

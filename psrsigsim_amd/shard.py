@@ -89,8 +89,12 @@ class RowSet(object):
         # the reductions run on CPU tensors: the group needs a host backend
         # (an NCCL/RCCL group would fail or hang here; bench.py makes a gloo
         # group next to the RCCL one)
+        if not dist.is_available() or not dist.is_initialized():
+            raise ValueError("plan_group needs an initialised torch.distributed process group (gloo): call "
+                             "torch.distributed.init_process_group first")
         backend = str(dist.get_backend(group)).lower()
-        if backend not in ("gloo", "mpi"):
+        # a mixed-device group ('cpu:gloo,cuda:nccl') reduces CPU tensors on its gloo part
+        if not any(b in backend for b in ("gloo", "mpi")):
             raise ValueError("plan_group must be a CPU (gloo) process group, got backend %r: create one with "
                              "torch.distributed.new_group(backend='gloo')" % backend)
         self.c0, self.c1, self.nglobal, self.group = int(c0), int(c1), int(nglobal), group

@@ -22,7 +22,7 @@ def test_golden_replay(name, fused, hip_lib):
 
 
 SIZES = [64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536, 1 << 17, 1 << 18,
-         1 << 20, 244, 1000, 30720,
+         1 << 20, 1 << 23, 244, 1000, 30720,
          # mixed-radix four-step: N1 x N2 = 6 x 2048, 10 x 4096, 30 x 2048, 30 x 4096, 24 x 8192
          12288, 40960, 61440, 122880, 196608,
          # Bluestein (chirp-z) fallback: M1 x M2 = 8 x 4096 (2 x 5003), 64 x 4096,
@@ -116,6 +116,12 @@ def test_null_tied_channel0_raises_on_every_readout(hip_lib):
     for _ in range(2):
         with pytest.raises(ValueError):
             sig.data
+    # new pulses replace the data: the earlier null's error no longer applies
+    # (ADVICE r03), as with the reference, which raised once at null() time
+    import torch
+    psr.make_pulses(sig, n * 20.48e-6)
+    d = sig.data
+    assert d.shape == (2, n) and bool(torch.isfinite(d).all())
 
 
 def _big_case(log2n, nchan, null=True, fd=True):

@@ -194,10 +194,12 @@ def test_bench_self_launch_world2():
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    for scaling in ("weak", "strong"):
+    for scaling in ("weak", "strong", None):
+        flag = ["--scaling", scaling] if scaling else []
         r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1",
-                            "--warmup", "0", "--dry-run", "--log2n", "14", "--nchan", "8", "--scaling", scaling],
+                            "--warmup", "0", "--dry-run", "--log2n", "14", "--nchan", "8"] + flag,
                            capture_output=True, text=True, timeout=300, cwd=root)
+        scaling = scaling or "strong"      # the C3 default: one signal split over the GPUs (BASELINE C3)
         assert r.returncode == 0, r.stderr[-2000:]
         lines = [l for l in r.stdout.splitlines() if l.strip()]
         assert len(lines) == 1 and lines[0].startswith("{"), r.stdout   # stdout carries only the JSON line
@@ -213,6 +215,22 @@ def test_rowset_requires_host_backend(monkeypatch):
     """shard.RowSet reduces CPU tensors: an NCCL/RCCL plan_group is refused
     with a clear error instead of failing or hanging inside a collective."""
     from psrsigsim_amd import shard
+    monkeypatch.setattr(shard.dist, "is_initialized", lambda: True)
     monkeypatch.setattr(shard.dist, "get_backend", lambda group=None: "nccl")
     with pytest.raises(ValueError, match="gloo"):
         shard.RowSet(0, 4, 4, object())
+
+
+def test_rowset_uninitialised_and_mixed_backend(monkeypatch):
+    """Without an initialised process group RowSet raises a ValueError
+    naming the fix; a mixed-device group ('cpu:gloo,cuda:nccl') is accepted
+    (its gloo part reduces the CPU tensors)."""
+    from psrsigsim_amd import shard
+    monkeypatch.setattr(shard.dist, "is_initialized", lambda: False)
+    with pytest.raises(ValueError, match="init_process_group"):
+        shard.RowSet(0, 4, 4, None)
+    monkeypatch.setattr(shard.dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(shard.dist, "get_backend", lambda group=None: "cpu:gloo,cuda:nccl")
+    monkeypatch.setattr(shard, "_COVERED", {(id(None), 0, 4, 4)})
+    rs = shard.RowSet(0, 4, 4, None)
+    assert rs.c0 == 0 and rs.c1 == 4
