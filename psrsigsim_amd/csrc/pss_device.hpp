@@ -39,13 +39,7 @@ __device__ __forceinline__ cf csub(cf a, cf b) { return make_float2(a.x - b.x, a
 // v_cos_f32 (input in revolutions; measured max abs error 1.2e-7 on MI355X,
 // tools/probe_trig.hip).  |r| <= 0.5 keeps the argument's own rounding small.
 __device__ __forceinline__ cf expi_rev(float r) {
-#ifdef PSS_ACCURATE_TRIG
-    float s, c;
-    sincospif(2.0f * r, &s, &c);
-    return make_float2(c, s);
-#else
     return make_float2(__builtin_amdgcn_cosf(r), __builtin_amdgcn_sinf(r));
-#endif
 }
 
 // 2^-64-cycle fixed point phase -> signed revolutions in [-0.5, 0.5).
@@ -112,18 +106,20 @@ struct Buf {
 };
 
 // --------------------------------------------------------------------------
-// Philox4x32-7 (Salmon et al., SC'11).  7 rounds is the round count the
-// Random123 paper reports as passing BigCrush for Philox4x32 (10 is its
-// default safety margin).  The step is power-throttled and issue-bound, so the
-// 3 rounds (12 VALU per 4 draws) are worth 0.9 ms at C3; the distribution
-// gates (KS / moments, tests/test_gpu_stats.py) guard the generator.
+// Philox4x32-7 (Salmon et al., SC'11, "Parallel random numbers: as easy as
+// 1, 2, 3"): Philox4x32 with 7 rounds is the fewest their paper reports as
+// passing TestU01's BigCrush (Table 2); Random123 defaults to 10 as a safety
+// margin.  The step is issue-bound and power-throttled, and the 3 rounds (12
+// VALU per 4 draws) are worth 0.9 ms at C3.  This is part of the stream
+// definition: changing kPhiloxRounds changes every draw (DESIGN.md section 4
+// and INTEGRATION.md record it); the distribution gates (KS / moments,
+// tests/test_gpu_stats.py) and tools/philox_model.py's 400-seed study
+// (profiles/r03/philox_quality.txt) guard the generator.
 // --------------------------------------------------------------------------
-#ifndef PSS_PHILOX_ROUNDS
-#define PSS_PHILOX_ROUNDS 7
-#endif
+static constexpr int kPhiloxRounds = 7;
 __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-    for (int r = 0; r < PSS_PHILOX_ROUNDS; ++r) {
+    for (int r = 0; r < kPhiloxRounds; ++r) {
         // one v_mad_u64_u32 per product (hi and lo together), not mul_hi + mul_lo
         const uint64_t p0 = (uint64_t)c.x * 0xD2511F53u;
         const uint64_t p1 = (uint64_t)c.z * 0xCD9E8D57u;
@@ -158,11 +154,7 @@ __device__ __forceinline__ float u01(uint32_t x) {
 // shift-or and one subtract, both full rate; v_cvt_f32_u32 issues at half
 // rate on gfx950, tools/probe_rates.hip).  Exact: 23-bit grid of [0, 1).
 __device__ __forceinline__ float frac23(uint32_t x) {
-#ifdef PSS_OLD_CVT   // A/B switch (tools/ablate.sh): the v_cvt form, 24 bits
-    return (float)(x >> 8) * 5.9604644775390625e-08f;
-#else
     return __uint_as_float(0x3F800000u | (x >> 9)) - 1.0f;
-#endif
 }
 
 // Four chi2(1) draws from one Philox block: z^2 with z Box-Muller normals,
@@ -174,14 +166,10 @@ __device__ __forceinline__ float frac23(uint32_t x) {
 // small member of the pair is resolved to ~ulp(h) = h 6e-8 absolute
 // (chi2 values below ~1e-6; the distribution gates, tests/test_gpu_stats.py,
 // cover the sampler).
-#ifndef PSS_BM_ONE_TRIG
-#define PSS_BM_ONE_TRIG 1
-#endif
 // `scale` multiplies the draws inside the sampler (h scale = (-ln2 scale)
 // log2 u: the product with the pulse draw_norm costs no extra instruction);
 // scale = 1 gives the plain chi2(1) values.
 __device__ __forceinline__ float4 chi2_1x4(uint4 r, float scale = 1.0f) {
-#if PSS_BM_ONE_TRIG
     const float kl = -0.6931471805599453f * scale;
     const float h0 = kl * __builtin_amdgcn_logf(u01(r.x));   // -ln u = -ln2 log2 u
     const float h1 = kl * __builtin_amdgcn_logf(u01(r.z));
@@ -189,15 +177,6 @@ __device__ __forceinline__ float4 chi2_1x4(uint4 r, float scale = 1.0f) {
     const float c1 = __builtin_amdgcn_cosf(frac23(r.w << 1));
     const float t0 = h0 * c0, t1 = h1 * c1;
     return make_float4(h0 + t0, h0 - t0, h1 + t1, h1 - t1);
-#else
-    float l0 = -1.3862943611198906f * __builtin_amdgcn_logf(u01(r.x));   // -2 ln u = -2 ln2 log2 u
-    float l1 = -1.3862943611198906f * __builtin_amdgcn_logf(u01(r.z));
-    float v0 = frac23(r.y);                                              // [0,1) revolutions
-    float v1 = frac23(r.w);
-    float c0 = __builtin_amdgcn_cosf(v0), s0 = __builtin_amdgcn_sinf(v0);
-    float c1 = __builtin_amdgcn_cosf(v1), s1 = __builtin_amdgcn_sinf(v1);
-    return make_float4(l0 * c0 * c0 * scale, l0 * s0 * s0 * scale, l1 * c1 * c1 * scale, l1 * s1 * s1 * scale);
-#endif
 }
 
 // Four N(0, 1) draws from one Philox block (Box-Muller pairs

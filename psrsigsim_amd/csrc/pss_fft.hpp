@@ -232,13 +232,10 @@ struct RegDft<1, INV> {
 // banks: 2x the cycles, tools/lds_banks.py); row pitch RS = L + XRS, XRS
 // chosen per kernel for its cross-row (transposing) accesses.  Other L (the
 // mixed-radix columns 6..60): pad of one complex per 16.
-#ifndef PSS_LDS_PAD
-#define PSS_LDS_PAD 0      // experiment switch: 1 = the round-1 padded layout everywhere
-#endif
 template <int L, int XRS = 1>
 struct Lds {
     // XRS < 0: the padded layout (a kernel whose accesses it suits better)
-    static constexpr bool SWZ = (L % 16) == 0 && !PSS_LDS_PAD && XRS >= 0;
+    static constexpr bool SWZ = (L % 16) == 0 && XRS >= 0;
     // row pitch (complex); the padded pitch is odd so that accesses across
     // rows (one position of many sequences) spread over the banks
     static constexpr int RS = SWZ ? L + XRS : ((L + L / 16 + 1) | 1);
@@ -260,10 +257,7 @@ struct RList {};
 // (the index form costs an XOR and a shift-add per value), and gathers with a
 // stride that is a multiple of 256 positions are a base plus immediate
 // offsets.  Fft<..., XRS> selects it when Lds<L, XRS>::RS % 16 == 0
-// (PSS_LDS_XB); the caller then owes the 128-B alignment of the buffer.
-#ifndef PSS_LDS_XB
-#define PSS_LDS_XB 1
-#endif
+// (Fft::XB); the caller then owes the 128-B alignment of the buffer.
 typedef float lds_f2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) lds_f2 lds_f2_t;
 __device__ __forceinline__ uint32_t lds_byte(const cf *p) {
@@ -300,9 +294,6 @@ __device__ __forceinline__ void stage_sync() {
 // e^{-2 pi i k q / 256}, k, q < 16 (row pitch 17: rows start on different
 // banks).  Filled once per workgroup from kCos256 (correctly rounded fp32,
 // below the native sincos' 1.2e-7 error).
-#ifndef PSS_TW16
-#define PSS_TW16 1      // experiment switch: 0 = native-sincos twiddles in every stage
-#endif
 static constexpr int kTw16Pitch = 17;
 static constexpr int kTw16Size = 16 * kTw16Pitch;
 // cos(2 pi m / 256), m = 0..255, correctly rounded to fp32 (float64 cos;
@@ -383,7 +374,7 @@ template <int L, int BATCH, int T, bool WAVE = false, int XRS = 1>
 struct Fft {
     using LD = Lds<L, XRS>;
     // byte-address forms of the exchanges (see lds_byte)
-    static constexpr bool XB = PSS_LDS_XB && LD::SWZ && (LD::RS % 16 == 0);
+    static constexpr bool XB = LD::SWZ && (LD::RS % 16 == 0);
     static constexpr int E = L * BATCH / T;
     static_assert(E * T == L * BATCH, "T must divide L*BATCH");
     static_assert(!WAVE || (T == 64 && BATCH == 1), "a wave-local transform is one sequence on 64 lanes");
@@ -430,7 +421,7 @@ struct Fft {
     // Run the stage list.  Ns = product of the radices already applied.
     template <bool INV, int Ns, int R, int... Rest>
     __device__ static __forceinline__ void run(cf (&v)[E], cf *lds, int tid) {
-        run_impl<INV, false, false, 0, Ns, R, Rest...>(v, lds, tid, nullptr, nullptr);
+        run_impl<INV, false, false, Ns, R, Rest...>(v, lds, tid, nullptr);
     }
     // The same with the radix-16 stage after a radix-16 stage (Ns = 16: the
     // 15 twiddles w^q, w = e^{-+2 pi i k/256}, k < 16) read from the table
@@ -438,17 +429,7 @@ struct Fft {
     // 4 native sincos + 11 products per butterfly.
     template <bool INV, int Ns, int R, int... Rest>
     __device__ static __forceinline__ void run_tw(cf (&v)[E], cf *lds, int tid, const cf *tw16) {
-        run_impl<INV, PSS_TW16 != 0, false, 0, Ns, R, Rest...>(v, lds, tid, tw16, nullptr);
-    }
-    // run_tw with the last stage's native-sincos twiddles kept in registers:
-    // CM = 1 (forward) saves w^H, w, w^2 .. w^(H-1) (twc[0 .. H-1]) when the
-    // thread has one butterfly per stage (E == R); CM = 2 (inverse, same
-    // thread, the SAME palindromic radix list) takes their conjugates instead
-    // of 4 native sincos and 4 products per butterfly -- the row pass's
-    // inverse after its forward.
-    template <bool INV, int CM, int Ns, int R, int... Rest>
-    __device__ static __forceinline__ void run_tw_c(cf (&v)[E], cf *lds, int tid, const cf *tw16, cf *twc) {
-        run_impl<INV, PSS_TW16 != 0, false, CM, Ns, R, Rest...>(v, lds, tid, tw16, twc);
+        run_impl<INV, true, false, Ns, R, Rest...>(v, lds, tid, tw16);
     }
 
     // Every stage but the last, then the exchange into the last stage's input
@@ -457,11 +438,11 @@ struct Fft {
     template <bool INV, int Ns, int R, int... Rest>
     __device__ static __forceinline__ void run_head_tw(cf (&v)[E], cf *lds, int tid, const cf *tw16) {
         static_assert(sizeof...(Rest) >= 1, "run_head_tw needs at least two stages");
-        run_impl<INV, PSS_TW16 != 0, true, 0, Ns, R, Rest...>(v, lds, tid, tw16, nullptr);
+        run_impl<INV, true, true, Ns, R, Rest...>(v, lds, tid, tw16);
     }
 
-    template <bool INV, bool TW, bool HEAD, int CM, int Ns, int R, int... Rest>
-    __device__ static __forceinline__ void run_impl(cf (&v)[E], cf *lds, int tid, const cf *tw16, cf *twc) {
+    template <bool INV, bool TW, bool HEAD, int Ns, int R, int... Rest>
+    __device__ static __forceinline__ void run_impl(cf (&v)[E], cf *lds, int tid, const cf *tw16) {
         static_assert(E % R == 0, "E must be a multiple of every radix");
         constexpr int LR = L / R;
 #pragma unroll
@@ -480,42 +461,17 @@ struct Fft {
                 constexpr int H = (R >= 8) ? R / 2 : R;   // powers kept: w^1 .. w^(H-1)
                 cf w[H];
                 const float base = (float)k * (1.0f / (float)(Ns * R));   // [0, 1/R)
-                // twiddle cache (run_tw_c): this stage's powers from the forward pass
-                // (the last stage only: with a palindromic radix list -- the
-                // caller's contract -- it has the same Ns and k in both passes)
-                constexpr bool kCache = CM != 0 && E == R && sizeof...(Rest) == 0 && !(TW && Ns == 16 && R == 16);
-#if defined(PSS_ABLATE) && (PSS_ABLATE & 32)
-                // ablation: twiddles without generation cost (wrong values)
 #pragma unroll
-                for (int q = 1; q < R; ++q) a[q] = cmul(a[q], make_float2(base, (float)q));
-                if (true) { dft<R, INV>(a); continue; }
-#endif
-                if constexpr (kCache && CM == 2) {
+                for (int p2 = 1; p2 < H; p2 *= 2) w[p2] = expi_rev(INV ? p2 * base : -p2 * base);
 #pragma unroll
-                    for (int q = 1; q < H; ++q) w[q] = make_float2(twc[q].x, -twc[q].y);
-                } else {
-#pragma unroll
-                    for (int p2 = 1; p2 < H; p2 *= 2) w[p2] = expi_rev(INV ? p2 * base : -p2 * base);
-#pragma unroll
-                    for (int q = 3; q < H; ++q) {
-                        const int hi = 1 << (31 - __builtin_clz(q));   // compile-time after unrolling
-                        if (q != hi) w[q] = cmul(w[hi], w[q - hi]);
-                    }
-                    if constexpr (kCache && CM == 1) {
-#pragma unroll
-                        for (int q = 1; q < H; ++q) twc[q] = w[q];
-                    }
+                for (int q = 3; q < H; ++q) {
+                    const int hi = 1 << (31 - __builtin_clz(q));   // compile-time after unrolling
+                    if (q != hi) w[q] = cmul(w[hi], w[q - hi]);
                 }
 #pragma unroll
                 for (int q = 1; q < H; ++q) a[q] = cmul(a[q], w[q]);
                 if constexpr (H < R) {
-                    cf wh;
-                    if constexpr (kCache && CM == 2) {
-                        wh = make_float2(twc[0].x, -twc[0].y);
-                    } else {
-                        wh = expi_rev(INV ? H * base : -H * base);
-                        if constexpr (kCache && CM == 1) twc[0] = wh;
-                    }
+                    const cf wh = expi_rev(INV ? H * base : -H * base);
                     a[H] = cmul(a[H], wh);
 #pragma unroll
                     for (int q = 1; q < H; ++q) a[H + q] = cmul(a[H + q], cmul(wh, w[q]));
@@ -558,7 +514,7 @@ struct Fft {
             constexpr int R2 = first<Rest...>();
             load<R2>(v, lds, tid);
             stage_sync<WAVE>();
-            if constexpr (!(HEAD && sizeof...(Rest) == 1)) run_impl<INV, TW, HEAD, CM, Ns * R, Rest...>(v, lds, tid, tw16, twc);
+            if constexpr (!(HEAD && sizeof...(Rest) == 1)) run_impl<INV, TW, HEAD, Ns * R, Rest...>(v, lds, tid, tw16);
         }
     }
 

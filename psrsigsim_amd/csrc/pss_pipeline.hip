@@ -21,161 +21,16 @@
 #include "pss_fft.hpp"
 #include "../../include/pss_hip.h"
 
-// Diagnostic ablations (tools/ablate.sh): PSS_ABLATE bits switch parts of the
-// pair-mode kernels off to attribute their cost.  0 in every product build.
-#ifndef PSS_ABLATE
-#define PSS_ABLATE 0
-#endif
-static constexpr int kAbl = PSS_ABLATE;
-// Layout experiments (tools/ablate.sh): XCD-aware column-block order, and the
-// 1024 x 4096 four-step split for N = 2^22 instead of 512 x 8192.
-#ifndef PSS_XCD_MAP
-#define PSS_XCD_MAP 1
-#endif
-#ifndef PSS_SPLIT4K
-#define PSS_SPLIT4K 1
-#endif
-static constexpr bool kXcdMap = PSS_XCD_MAP != 0;
-static constexpr bool kSplit4k = PSS_SPLIT4K != 0;
-// fast pass C block width / threads for N = 2^22 (1024 x 4096 split)
-#ifndef PSS_ROW4K   // 2^17..2^21: rows of 4096 instead of 8192
-#define PSS_ROW4K 1
-#endif
-#ifndef PSS_MASK_SIDE   // build the delayed-null mask table on a side stream next to pass A
-#define PSS_MASK_SIDE 1
-#endif
-#ifndef PSS_BC
-#define PSS_BC 16
-#define PSS_TC 1024
-#endif
-// pass A: PCHIP interval / fraction of consecutive samples by increments
-// (PhaseWalk) instead of per-sample multiplies (experiment switch)
-#ifndef PSS_PHASE_WALK
-#define PSS_PHASE_WALK 1
-#endif
-// column FFTs of passes A / C wave-local (one wave per column, no workgroup
-// barriers between stages); experiment switch
-#ifndef PSS_WAVE_COLS
-#define PSS_WAVE_COLS 1
-#endif
-// C5's 2048 x 8192 split: pass C too with one wave per 8-column block's
-// column (512 threads; experiment switch, measured slower)
-#ifndef PSS_C5_WAVE
-#define PSS_C5_WAVE 0
-#endif
-// C5: pass C with 16-column blocks (64-B output segments instead of 32) held in
-// registers between LDS phases, 2 columns per wave (passC_fast32)
-#ifndef PSS_C5_WIDE
-#define PSS_C5_WIDE 1
-#endif
-// 8192-point data rows (C5) one row at a time through LDS, both in
-// registers, two workgroups per CU (PairRowsSeq)
-#ifndef PSS_ROW_SEQ
-#define PSS_ROW_SEQ 1
-#endif
-// the same for C3's 4096-point rows (256 threads, up to 4 workgroups per CU;
-// experiment switch).  Measured (profiles/r03/s18, s19, same box): row
-// 19.6-19.7 ms with radix 16^3 (36 VGPRs spilled), 17.4-17.5 ms with 8^4
-// (PSS_ROW8=1); with row B's thread relabelling (no mirror exchanges)
-// 16.8 / 17.0 ms -- against 15.3-15.5 ms for both rows in LDS at two
-// workgroups per CU
-#ifndef PSS_ROW_SEQ4K
-#define PSS_ROW_SEQ4K 0
-#endif
-// row pass of the 1024 x 4096 split with 1024 threads (8 values each, radix
-// 8^4) for 8 waves per SIMD instead of 4 (experiment switch).  Measured
-// (profiles/r03/s12, same box): row 21.2-21.3 ms against 15.3-15.4 -- at the
-// 64-VGPR budget of 8 waves the kernel spills 12 VGPRs, and the fourth
-// radix-8 stage adds an LDS exchange
-#ifndef PSS_ROW8
-#define PSS_ROW8 0
-#endif
-// fast pass C with 32-column blocks held in registers between LDS phases
-// (passC_fast32; the C3 1024 x 4096 split only); experiment switch.  Measured
-// (profiles/r03/s11, same box): pass C 16.86-16.89 ms against 16.75-16.81 --
-// the two register-held columns push the 1024-thread kernel to the 128-VGPR
-// cap and 20 VGPRs spill around the FFTs; bitwise equal (146 GPU tests).  The
-// 512-thread form (4 columns per wave, 235 VGPRs, no spill, 2 waves per
-// SIMD): 16.80-16.83 against 16.44-16.50 (profiles/r03/s13) -- the wider
-// output segments do not pay for the extra phases at this occupancy
-#ifndef PSS_PC32
-#define PSS_PC32 0
-#endif
-#ifndef PSS_PC32_T     // its threads: 1024 (2 columns per wave) or 512 (4 per wave, 256 VGPRs)
-#define PSS_PC32_T 512
-#endif
-// fast pass C: column blocks per workgroup (2: the two halves of each 128-B
-// output line stored by the same lane back to back; 1: one block); experiment switch
-#ifndef PSS_PC_NBLK
-#define PSS_PC_NBLK 1
-#endif
-// pass A: the four-step twiddle folded into the last column-FFT stage (1) or
-// applied after the FFT (0); experiment switch
-#ifndef PSS_MERGE_TW
-#define PSS_MERGE_TW 1
-#endif
-// delayed-null fix-up over the list of table words with nulls (1) or over
-// every word of every channel (0); experiment switch
-// row pass: keep the last forward stage's twiddles in registers for the
-// inverse (experiment switch)
-#ifndef PSS_ROW_TWC
-#define PSS_ROW_TWC 0
-#endif
-#ifndef PSS_NULL_LIST
-#define PSS_NULL_LIST 1
-#endif
-// cache policy bits of the column passes' spill loads (experiment switch;
-// gfx950 buffer aux: 1 = sc0, 2 = nt, 16 = sc1)
-#ifndef PSS_SPILL_AUX
-#define PSS_SPILL_AUX 0
-#endif
-// Pair spill layout.  1: the two rows {k1, N1 - k1} ({0, N1/2}) that one
-// row-pass workgroup transforms together are interleaved sample by sample,
-// complex index (p N2 + n2) 2 + side (il_row below): pass A writes, and pass
-// C reads, one contiguous segment of 2 B complex per row pair instead of B
-// per row, and the row pass reads one contiguous block.  0: row-major
-// [k1][n2] (experiment switch).
-#ifndef PSS_PAIR_IL
-#define PSS_PAIR_IL 0
-#endif
-static constexpr bool kPairIL = PSS_PAIR_IL != 0;
-// row k1 of side `side` of interleaved row pair p
-__device__ __forceinline__ int il_row(int p, int side, int N1) {
-    return side == 0 ? p : (p == 0 ? N1 / 2 : N1 - p);
-}
-// Padding of each pair-spill row (complex) on the power-of-two split: the
-// rows' starts then do not all fall on the same HBM channel (experiment
-// switch; the mixed-radix split shares fallback bytes and keeps no pad).
-#ifndef PSS_SPILL_PAD
-#define PSS_SPILL_PAD 0
-#endif
-static constexpr int kSpillPad = PSS_SPILL_PAD;
-// cache policy bits of the fast pass C's output stores (experiment switch;
-// gfx950 buffer aux: 1 = sc0, 2 = nt, 16 = sc1)
-#ifndef PSS_OUT_AUX
-#define PSS_OUT_AUX 0
-#endif
-// Delayed null fused into the fast pass C (1): each item looks its 4 samples
-// up in the mask table and stores replacement + noise where nulled, so no
-// separate fix-up pass rewrites them; 0 (product): k_null_fix_list
-// afterwards.  Measured (C3, one box): fused pass C 27.0 ms against 16.6 +
-// 2.5 for pass C + fix-up -- the per-lane table lookups 8192 samples apart
-// and the f-dependent positions, divergent in every wave, cost far more than
-// the fix-up's compacted pass (bitwise the same results; 138 GPU tests).
-#ifndef PSS_FUSE_NULL
-#define PSS_FUSE_NULL 0
-#endif
-static constexpr bool kFuseNull = PSS_FUSE_NULL != 0;
-// pass A's spill stores non-temporal (experiment switch)
-#ifndef PSS_SPILL_NT
-#define PSS_SPILL_NT 0
-#endif
-// fast pass C block width / threads for N = 2^22 on the 512 x 8192 split
-#ifndef PSS_BC8
-#define PSS_BC8 16
-#define PSS_TC8 512
-#endif
-
+// Fixed product choices (each measured against its alternatives, DESIGN.md
+// sections 3 and 10; the rejected variants live in the git history):
+//   * column blocks of the column passes mapped XCD-contiguously (xcd_block);
+//   * 2^22 split 1024 x 4096 (rows of 4096 for 2^17 .. 2^22), 2^24 split
+//     2048 x 8192;
+//   * fast pass C on 16-column blocks of 1024 threads (C3), 16-column
+//     register-resident blocks of 512 threads (C5, passC_fast32);
+//   * the delayed-null mask table built on a side stream next to pass A, and
+//     applied by the compacted fix-up (k_null_fix_list) after pass C.
+static constexpr int kBC = 16, kTC = 1024;   // fast pass C block / threads (C3 and 2^17 .. 2^21)
 
 using namespace pss;
 
@@ -247,7 +102,6 @@ struct KP {
     // four-step pair mode (two channels per complex row)
     int npairs;
     int poff;       // chan0 & 1: pairs are (even, odd) GLOBAL channels
-    int64_t sp;     // pair spill row pitch (complex; 0 = N2): N2 + PSS_SPILL_PAD on the 2^m split
     cf *Yd;         // data pair spill    [npairs][N1][sp]
     cf *Ym;         // node pair spill    [KCH/2][N1][N2] (mask table build)
     const cf *Mspec;// mask spectrum      [N1][N2] (natural k2 per row k1)
@@ -260,13 +114,12 @@ struct KP {
     const uint32_t *mbits;  // [nchan][N/32] per-channel null decisions (k_mask_bits)
     int mbB;                // column-block width B of pass C (mbits layout)
     const cf *rtab;         // [npairs][RFL][2] row-pass pair ramp factors {E, D} (k_pair_tab)
-    hipEvent_t after_a;     // batching: recorded after this launch's pass A (or NULL)
     hipEvent_t mask_ready;  // mask table built on a side stream: wait before its first use (or NULL)
     const uint32_t *wlist;  // delayed null: table words with a nulled position (any f)
     const uint32_t *nwlist; // its length (device)
 };
 // pair spill row pitch and per-pair stride (complex)
-__host__ __device__ __forceinline__ int64_t rpitch(const KP &k) { return k.sp ? k.sp : k.N2; }
+__host__ __device__ __forceinline__ int64_t rpitch(const KP &k) { return k.N2; }
 __host__ __device__ __forceinline__ int64_t pstride(const KP &k) { return k.N1 * rpitch(k); }
 
 
@@ -389,7 +242,7 @@ __device__ __forceinline__ uint32_t mask_run(const KP &k, uint32_t n, uint32_t i
     const uint32_t msk = RUN >= 32u ? 0xffffffffu : ((1u << RUN) - 1u);
     uint32_t r32 = (uint32_t)(((((uint64_t)Bw.x) << 32) | A.x) >> sh) & msk;
     uint32_t amb = (uint32_t)(((((uint64_t)Bw.y) << 32) | A.y) >> sh) & msk;
-    if (!amb || (kAbl & 256)) return r32;       // (ablation 256: no f-dependent evaluations)
+    if (!amb) return r32;
     // Ambiguous positions cluster at pulse edges (a lane may hold ~20): take
     // them four at a time so the coefficient loads of a group are in flight
     // together instead of one exposed latency per position (the table bases
@@ -448,61 +301,6 @@ __global__ __launch_bounds__(256) void k_mask_bits(KP k, uint32_t *bm) {
         out |= mask_run(k, n, is, t, RUN) << s;
     }
     bm[(int64_t)r * (wm + 1u) + j] = out;
-}
-
-// Delayed null on the fast path (see passC_fast): after pass C stored every
-// sample as signal + noise, rewrite the nulled ones as replacement + noise --
-// the same Philox draws and expression as epilogue4, so the result is bitwise
-// that of the generic kernels.  One thread per 32-sample word, natural order:
-// ~90% of the words have no nulled sample and only read two table words.  A
-// nulled pulse covers ~8 words, so the nulled 4-sample groups of a wave are
-// listed in LDS first and then drawn 64 at a time (one Philox pair per lane
-// per round) instead of up to 8 rounds in the lanes that hold them.
-__global__ __launch_bounds__(256) void k_null_fix(KP k) {
-    __shared__ uint32_t desc[4][64 * 8];
-    const int r = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
-    const PssPipeline &p = k.p;
-    uint32_t is;
-    float t;
-    mask_split((uint64_t)p.mask_ramp[r], k.log2n, is, t);
-    const uint32_t hits = (j <= (((uint32_t)k.N - 1u) >> 5)) ? mask_run(k, j << 5, is, t, 32u) : 0u;
-    if (__ballot(hits != 0u) == 0ull) return;                     // wave-uniform
-    // entry = source lane << 8 | group << 4 | 4-bit decisions
-    const uint64_t below = (1ull << lane) - 1ull;
-    uint32_t total = 0;
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {
-        const uint32_t h = (hits >> (4 * g)) & 15u;
-        const uint64_t bal = __ballot(h != 0u);
-        if (h) desc[wv][total + (uint32_t)__popcll(bal & below)] = ((uint32_t)lane << 8) | ((uint32_t)g << 4) | h;
-        total += (uint32_t)__popcll(bal);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint32_t c = (uint32_t)(p.chan0 + r);
-    float *row = p.data + (int64_t)r * p.ld;
-    const Rng gn(p.seed, p.call_noise, P_NOISE), gr(p.seed, p.call_null, P_REP);
-    const float nn = p.noise_norm, sc = p.null_rep_scale;
-    for (uint32_t e = (uint32_t)lane; e < total; e += 64u) {
-        const uint32_t d = desc[wv][e], h = d & 15u;
-        const int64_t n = ((int64_t)(j - (uint32_t)lane + (d >> 8)) << 5) + 4 * ((d >> 4) & 15u);
-        const float4 xn = chi2_1x4(gn.bits((uint32_t)(n >> 2), c, (uint32_t)(n >> 34)));
-        const float4 xr = chi2_1x4(gr.bits((uint32_t)(n >> 2), c, (uint32_t)(n >> 34)));
-        const float vn[4] = {xn.x, xn.y, xn.z, xn.w}, vr[4] = {xr.x, xr.y, xr.z, xr.w};
-        if (h == 15u) {
-            // whole group nulled (the interior of a pulse): one 16-B store
-            // (fast path only: ld % 4 == 0 and a 16-B aligned base)
-            *reinterpret_cast<float4 *>(row + n) =
-                make_float4(fmaf(nn, vn[0], vr[0] * sc), fmaf(nn, vn[1], vr[1] * sc),
-                            fmaf(nn, vn[2], vr[2] * sc), fmaf(nn, vn[3], vr[3] * sc));
-            continue;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if ((h >> i) & 1u) row[n + i] = fmaf(nn, vn[i], vr[i] * sc);
-    }
 }
 
 // Table words (32 positions each) that hold a position nulled for some f:
@@ -642,7 +440,7 @@ __device__ __forceinline__ void static_for(F &&f) {
 __device__ __forceinline__ void xcd_block(int &bx, int &by) {
     const uint32_t gx = gridDim.x, total = gx * gridDim.y;
     const uint32_t id = blockIdx.x + blockIdx.y * gx;
-    const uint32_t l = (kXcdMap && (total & 7u) == 0u) ? (id & 7u) * (total >> 3) + (id >> 3) : id;
+    const uint32_t l = ((total & 7u) == 0u) ? (id & 7u) * (total >> 3) + (id >> 3) : id;
     by = (int)(l / gx);
     bx = (int)(l - (uint32_t)by * gx);
 }
@@ -695,6 +493,34 @@ __device__ __forceinline__ void draw4(const Rng &g, int64_t n0, uint32_t c, floa
         chi2_pair(g, m, c, df, x[0], x[1]);
         chi2_pair(g, m + 1u, c, df, x[2], x[3]);
     }
+}
+
+// Search-mode chi2(1) pulse draw of sample n in a row of N samples (P_PULSE,
+// df = 1; `scale` = draw_norm folded into the sampler).  Keying: for N % 4
+// == 0 the Philox block m < N/4 holds samples m + e N/4 (e < 4, its four draws
+// in order) -- the rows n1, n1 + N1/4, n1 + N1/2, n1 + 3 N1/4 of one four-step
+// column, so a column's values are drawn where the column is transformed
+// (passA_wave: no cross-wave transpose of the generated samples); otherwise
+// block n >> 2 holds samples 4 (n >> 2) .. + 3.  Every path draws through this
+// rule (or the same blocks), so results do not depend on the path.
+__device__ __forceinline__ void pulse_block(int64_t n, int64_t N, uint32_t &m, uint32_t &tag, uint32_t &e) {
+    uint64_t mm;
+    if ((N & 3) == 0) {
+        const uint64_t Q = (uint64_t)N >> 2;
+        e = (uint32_t)((uint64_t)n / Q);
+        mm = (uint64_t)n - (uint64_t)e * Q;
+    } else {
+        mm = (uint64_t)n >> 2;
+        e = (uint32_t)(n & 3);
+    }
+    m = (uint32_t)mm;
+    tag = (uint32_t)(mm >> 32);
+}
+__device__ __forceinline__ float pulse_draw(const Rng &g, int64_t n, int64_t N, uint32_t c, float scale) {
+    uint32_t m, tag, e;
+    pulse_block(n, N, m, tag, e);
+    const float4 q = chi2_1x4(g.bits(m, c, tag), scale);
+    return e == 0u ? q.x : (e == 1u ? q.y : (e == 2u ? q.z : q.w));
 }
 
 // Interval index and fraction of sample n's pulse phase (shared by every
@@ -762,6 +588,14 @@ __device__ __forceinline__ void phase_delta(const PssPipeline &p, uint32_t &dlo,
     const uint64_t t = (uint64_t)(uint32_t)p.phase_step * p.knot_m;
     dlo = (uint32_t)t;
     dhi = (uint64_t)(uint32_t)(p.phase_step >> 32) * p.knot_m + (t >> 32);
+}
+// ... for a walk in strides of S samples: D = (S phase_step mod 2^64) knot_m
+// (exact: the walk's sum stays below 2 knot_m in the interval field)
+__device__ __forceinline__ void phase_delta_n(const PssPipeline &p, uint64_t S, uint32_t &dlo, uint64_t &dhi) {
+    const uint64_t ps = p.phase_step * S;
+    const uint64_t t = (uint64_t)(uint32_t)ps * p.knot_m;
+    dlo = (uint32_t)t;
+    dhi = (uint64_t)(uint32_t)(ps >> 32) * p.knot_m + (t >> 32);
 }
 
 __device__ __forceinline__ float pchip_row(const KP &k, int prow, uint32_t iv, float u) {
@@ -834,8 +668,13 @@ __device__ __forceinline__ void source4(const KP &k, int r, int64_t n0, int cnt,
                 // chi2(1) draws with draw_norm folded into the sampler (as the
                 // fast pass A draws them: bitwise the same values)
                 Rng g(p.seed, p.call_gen, P_PULSE);
-                const float4 q = chi2_1x4(g.bits((uint32_t)(n0 >> 2), c, (uint32_t)(n0 >> 34)), p.draw_norm);
-                x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
+                if ((k.N & 3) == 0) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[i] = (i < cnt) ? pulse_draw(g, n0 + i, k.N, c, p.draw_norm) : 0.f;
+                } else {
+                    const float4 q = chi2_1x4(g.bits((uint32_t)(n0 >> 2), c, (uint32_t)(n0 >> 34)), p.draw_norm);
+                    x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
+                }
                 dn = 1.0f;                                   // (x * 1 is exact)
             } else {
                 Rng g(p.seed, p.call_gen, P_PULSE);
@@ -1348,21 +1187,23 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
     static constexpr int LR = N2 / RF0;
     static constexpr int LRL = N2 / RFL;
     // minimum waves per SIMD the kernel is compiled for (VGPR budget 512 /
-    // waves): two workgroups per CU when two rows fit twice in LDS; the
-    // 1024-thread 4096-point variant (PSS_ROW8) aims at 8
-    static constexpr int kMinWaves = (T <= 512) ? 2 * T / 256 : (N2 <= 4096 ? 8 : 4);
-    // byte offset of (row, n2) in a pair spill (PSS_PAIR_IL: side b of row
-    // pair p), and the offset step of the q-th first-stage input (n2 + q LR)
-    static constexpr uint32_t kQS = (kPairIL ? 16u : 8u) * (uint32_t)LR;
-    __device__ static __forceinline__ uint32_t spill_off(uint32_t RP, int p, int row, int b, int n2) {
-        return kPairIL ? (((uint32_t)p * RP + (uint32_t)n2) * 2u + (uint32_t)b) * 8u
-                       : ((uint32_t)row * RP + (uint32_t)n2) * 8u;
+    // waves): two workgroups per CU when two rows fit twice in LDS
+    static constexpr int kMinWaves = (T <= 512) ? 2 * T / 256 : 4;
+    // byte offset of (row, n2) in a pair spill, and the offset step of the
+    // q-th first-stage input (n2 + q LR)
+    static constexpr uint32_t kQS = 8u * (uint32_t)LR;
+    __device__ static __forceinline__ uint32_t spill_off(uint32_t RP, int row, int n2) {
+        return ((uint32_t)row * RP + (uint32_t)n2) * 8u;
     }
 
     // MASK = false: data pair of channels (2pr - poff, 2pr + 1 - poff).
     // MASK = true : node pair (2pr, 2pr + 1) of the mask table build -- the
     //               once-per-run mask spectrum times each node's ramp.
-    template <bool MASK, bool TAIL = false>
+    // HT: a per-bin transfer function H (PssPipeline.htab: the baseband
+    // coherent dispersion, ism.py:76-98) instead of the delay ramps -- one H
+    // for every channel, so the packed pair's bins are simply H_ext(k) Z(k)
+    // (H_ext(N - k) = conj H(k); DC and Nyquist x Re H, the irfft rule).
+    template <bool MASK, bool TAIL = false, bool HT = false>
     __device__ static void pass(const KP &k) {
         __shared__ __align__(128) cf lds[2 * LD::RS];
         __shared__ cf tw16[kTw16Size];
@@ -1376,7 +1217,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
         const int ra = max(2 * pr - off, 0), rb = min(2 * pr + 1 - off, k.p.nchan - 1);
         const bool data = !MASK;
         const bool mask = MASK;
-        const uint64_t rwa = (uint64_t)k.p.ramp[ra], rwb = (uint64_t)k.p.ramp[rb];
+        const uint64_t rwa = HT ? 0ull : (uint64_t)k.p.ramp[ra], rwb = HT ? 0ull : (uint64_t)k.p.ramp[rb];
         // uniform 64-bit phase offsets of bin kb0 + q N/RFL relative to kb0 (SALU)
         const uint64_t sta = (uint64_t)(k.N / RFL) * rwa, stb = (uint64_t)(k.N / RFL) * rwb;
         const uint64_t nwa = (uint64_t)k.N * rwa, nwb = (uint64_t)k.N * rwb;
@@ -1388,17 +1229,29 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
 #pragma unroll
             for (int ib = 0; ib < E / RF0; ++ib) {
                 const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
-                const uint32_t off = spill_off(RP, j, b ? rowB : rowA, b, jj);
+                const uint32_t off = spill_off(RP, b ? rowB : rowA, jj);
 #pragma unroll
                 for (int q = 0; q < RF0; ++q) v[ib * RF0 + q] = Y.ld2(off, q * kQS);
             }
-            // the last stage's twiddles kept for the inverse (palindromic radix lists)
-            // (PSS_ROW_TWC: off by default -- its 16 live VGPRs across the ramp
-            // push the 4096-point kernel past the 128-VGPR cap of 4 waves per
-            // SIMD, and it measured neutral, profiles/r03/s3)
-            constexpr int kTwc = (PSS_ROW_TWC && std::is_same<RList<F...>, RList<I...>>::value) ? 2 : 0;
-            cf twc[8];
-            if constexpr (!(kAbl & 2)) FF::template run_tw_c<false, kTwc ? 1 : 0, 1, F...>(v, lds, tid, tw16, twc);
+            FF::template run_tw<false, 1, F...>(v, lds, tid, tw16);
+            if constexpr (HT) {
+                // bin kb0 + q N/RFL of butterfly ib (no mirror bins needed)
+                const cf *H = reinterpret_cast<const cf *>(k.p.htab);
+#pragma unroll
+                for (int ib = 0; ib < E / RFL; ++ib) {
+                    const int jg = tid + ib * T, b = jg / LRL, jj = jg - b * LRL;
+                    const int64_t kb0 = (b ? rowB : rowA) + (int64_t)N1 * jj;
+#pragma unroll
+                    for (int q = 0; q < RFL; ++q) {
+                        const int64_t kb = kb0 + (int64_t)q * (k.N / RFL);
+                        const bool upper = 2 * kb > k.N;
+                        const cf h = H[upper ? k.N - kb : kb];
+                        cf &z = v[ib * RFL + q];
+                        if (kb == 0 || 2 * kb == k.N) z = make_float2(z.x * h.x, z.y * h.x);
+                        else z = cmul(z, make_float2(h.x, upper ? -h.y : h.y));
+                    }
+                }
+            } else {
             FF::template store<RFL>(v, lds, tid);
             __syncthreads();
             // pair ramp factors (k_pair_tab): {E, D} per q, wave-uniform
@@ -1433,9 +1286,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                     const cf Sa = make_float2(Z.x + Zm.x, Z.y - Zm.y);
                     const cf Sb = make_float2(Z.y + Zm.y, Zm.x - Z.x);
                     cf W;
-                    if constexpr (kAbl & 8) {
-                        W = cadd(Sa, Sb);
-                    } else {
+                    {
                         const cf Ef = cmul(bE, ptab[2 * q]), Df = cmul(bD, ptab[2 * q + 1]);
                         if constexpr (TAIL) {
                             // per-channel transfer functions: R_a = E D, R_b = E conj(D)
@@ -1522,9 +1373,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                     // 2 D_a and 2 D_b (DC / Nyquist and the tail extension)
                     const cf Sa = make_float2(Z.x + Zm.x, Z.y - Zm.y);
                     const cf Sb = make_float2(Z.y + Zm.y, Zm.x - Z.x);
-                    if constexpr (kAbl & 8) {
-                        v[i] = cadd(Sa, Sb);
-                    } else if (kb0 == 0 && 2 * q == RFL) {          // Nyquist bin
+                    if (kb0 == 0 && 2 * q == RFL) {                 // Nyquist bin
                         float fa = k.p.nyq_re[ra], fb = k.p.nyq_re[rb];
                         if constexpr (TAIL) {                       // H(N/2) = (1-a)/(1+a)
                             const float ta = k.p.tail_a[ra], tb = k.p.tail_a[rb];
@@ -1555,12 +1404,13 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                 }
             }
             }
+            }   // (HT)
             __syncthreads();
-            if constexpr (!(kAbl & 2)) FF::template run_tw_c<true, kTwc, 1, I...>(v, lds, tid, tw16, twc);
+            FF::template run_tw<true, 1, I...>(v, lds, tid, tw16);
 #pragma unroll
             for (int ib = 0; ib < E / RF0; ++ib) {
                 const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
-                const uint32_t off = spill_off(RP, j, b ? rowB : rowA, b, jj);
+                const uint32_t off = spill_off(RP, b ? rowB : rowA, jj);
 #pragma unroll
                 for (int q = 0; q < RF0; ++q) Y.st2(v[ib * RF0 + q], off, q * kQS);
             }
@@ -1579,9 +1429,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                 for (int q = 0; q < RFL; ++q) {
                     const int i = ib * RFL + q;
                     const cf M = Ms.ld2(moff, q * LRL * 8);
-                    if constexpr (kAbl & 8) {
-                        v[i] = M;
-                    } else if (kb0 == 0 && 2 * q == RFL) {          // Nyquist bin
+                    if (kb0 == 0 && 2 * q == RFL) {                 // Nyquist bin
                         v[i] = make_float2(M.x * k.p.nyq_im[ra], M.x * k.p.nyq_im[rb]);
                     } else if (kb0 == 0 && q == 0) {                // DC: M (1 + i)
                         v[i] = make_float2(M.x - M.y, M.y + M.x);
@@ -1592,11 +1440,11 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                 }
             }
             __syncthreads();
-            if constexpr (!(kAbl & 2)) FF::template run_tw<true, 1, I...>(v, lds, tid, tw16);
+            FF::template run_tw<true, 1, I...>(v, lds, tid, tw16);
 #pragma unroll
             for (int ib = 0; ib < E / RF0; ++ib) {
                 const int jj0 = tid + ib * T, b = jj0 / LR, jj = jj0 - b * LR;
-                const uint32_t off = spill_off(RP, j, b ? rowB : rowA, b, jj);
+                const uint32_t off = spill_off(RP, b ? rowB : rowA, jj);
 #pragma unroll
                 for (int q = 0; q < RF0; ++q) V.st2(v[ib * RF0 + q], off, q * kQS);
             }
@@ -1604,13 +1452,13 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
     }
 };
 
-template <typename R, int T, bool TAIL = false>
-__global__ __launch_bounds__(T, R::kMinWaves) void k_pair_row(KP k) { R::template pass<false, TAIL>(k); }
+template <typename R, int T, bool TAIL = false, bool HT = false>
+__global__ __launch_bounds__(T, R::kMinWaves) void k_pair_row(KP k) { R::template pass<false, TAIL, HT>(k); }
 template <typename R, int T>
 __global__ __launch_bounds__(T) void k_node_row(KP k) { R::template pass<true>(k); }
 
 // Row pass of a data pair with the two rows of a row pair in registers and
-// ONE row in LDS (PSS_ROW_SEQ; the 8192-point rows of C5's 2048 x 8192
+// ONE row in LDS (the 8192-point rows of C5's 2048 x 8192
 // split): PairRows holds both rows in LDS (2 x 65.7 KB, one workgroup per
 // CU, so every barrier stalls the CU); here each exchange moves one row
 // through a 65.7-KB buffer and two workgroups share a CU.  Same stages and
@@ -1674,7 +1522,7 @@ struct PairRowsSeq<N2, T, RList<F...>, RList<I...>> {
         auto load = [&](cf (&v)[E], int row, int b, int t) __attribute__((always_inline)) {
 #pragma unroll
             for (int ib = 0; ib < E / RF0; ++ib) {
-                const uint32_t o = PRW::spill_off(RP, j, row, b, t + ib * T);
+                const uint32_t o = PRW::spill_off(RP, row, t + ib * T);
 #pragma unroll
                 for (int q = 0; q < RF0; ++q) v[ib * RF0 + q] = Y.ld2(o, q * PRW::kQS);
             }
@@ -1751,7 +1599,7 @@ struct PairRowsSeq<N2, T, RList<F...>, RList<I...>> {
 #pragma unroll
         for (int ib = 0; ib < E / RF0; ++ib) {
             const int jj = tid + ib * T;
-            const uint32_t oa = PRW::spill_off(RP, j, rowA, 0, jj);
+            const uint32_t oa = PRW::spill_off(RP, rowA, jj);
 #pragma unroll
             for (int q = 0; q < RF0; ++q) Y.st2(va[ib * RF0 + q], oa, q * PRW::kQS);
         }
@@ -1759,7 +1607,7 @@ struct PairRowsSeq<N2, T, RList<F...>, RList<I...>> {
 #pragma unroll
         for (int ib = 0; ib < E / RF0; ++ib) {
             const int jj = tb + ib * T;
-            const uint32_t ob = PRW::spill_off(RP, j, rowB, 1, jj);
+            const uint32_t ob = PRW::spill_off(RP, rowB, jj);
 #pragma unroll
             for (int q = 0; q < RF0; ++q) Y.st2(vb[ib * RF0 + q], ob, q * PRW::kQS);
         }
@@ -1784,9 +1632,9 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     // are wave-local (Fft<..., WAVE>: no workgroup barrier between stages);
     // only the transposes between sample-major items and columns need one.
     using FW = Fft<(N1 % 64 == 0 ? N1 : 64), 1, 64, true, XRS>;   // same row layout as LdsC (placeholder when N1 % 64 != 0)
-    static constexpr bool kWaveCols = PSS_WAVE_COLS && (T == 64 * B) && (N1 % 64 == 0) && (N1 / 64 == E);
+    static constexpr bool kWaveCols = (T == 64 * B) && (N1 % 64 == 0) && (N1 / 64 == E);
     // pass A: four-step twiddle folded into the column FFT's last stage
-    static constexpr bool kMergeTw = PSS_MERGE_TW && sizeof...(F) >= 2;
+    static constexpr bool kMergeTw = sizeof...(F) >= 2;
     static constexpr int RF0 = FF::template first<F...>();
     static constexpr int RFL = FF::template last_of<F...>();
     static constexpr int RI0 = FF::template first<I...>();
@@ -1827,7 +1675,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         const int pra = (p.prof_rows == 1) ? 0 : (int)ca - p.prof_row0, prb = (p.prof_rows == 1) ? 0 : (int)cb - p.prof_row0;
         const Rng g(p.seed, p.call_gen, P_PULSE);
         static_assert(!FAST || kItemsExact, "fast pass A: whole items per thread");
-        if constexpr (FAST && !(kAbl & 1)) {
+        if constexpr (FAST) {
             // The pair's two PCHIP rows are staged in LDS (host guarantees
             // nint <= kFastNint), the items are unrolled and branch-free, so
             // the table reads of an item issue together instead of one
@@ -1848,46 +1696,35 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             // draw_norm, or 0 for a pair's missing channel (shard / band
             // edges): the multiply the sample needs anyway zeroes it, no select
             const float dna = hasa ? p.draw_norm : 0.f, dnb = hasb ? p.draw_norm : 0.f;
-#if PSS_PHASE_WALK
+            // item = Philox block m = n1 N2 + n20 + b (n1 < N1/4): the samples
+            // m + e N/4 = rows n1 + e N1/4 of column b (pulse_draw's keying),
+            // their phases by a walk in strides of N/4
+            static_assert(N1 % 4 == 0, "fast pass A: quarter-row items");
+            constexpr int NQ = N1 / 4;
             uint32_t dlo;
             uint64_t dhi;
-            phase_delta(p, dlo, dhi);
+            phase_delta_n(p, (uint64_t)NQ * (uint64_t)N2, dlo, dhi);
             const uint32_t M = p.knot_m;
-#endif
 #pragma unroll
             for (int t = 0; t < ITEMS; ++t) {
-                // items along the column (lanes = consecutive rows n1 of one
-                // 4-column group): the transposed LDS writes below are
-                // conflict-free for any row pitch (this loop touches no
-                // global memory, so its item order is free)
+                // lanes = consecutive rows n1 of one column: the LDS writes
+                // below are conflict-free (this loop touches no global
+                // memory, so its item order is free)
                 const int it = tid + t * T;
-                int n1, b4;
-                if constexpr (N1 % 64 == 0) {
-                    n1 = it % N1;
-                    b4 = (it / N1) * 4;
-                } else {
-                    n1 = it / (B / 4);
-                    b4 = (it - n1 * (B / 4)) * 4;
-                }
-                const uint32_t n = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4;   // N <= 2^24
+                const int n1 = it % NQ, b = it / NQ;
+                const uint32_t m = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b;   // N <= 2^24
                 // draws scaled by draw_norm (0 for a pair's missing channel) in the sampler
-                const float4 qa = chi2_1x4(g.bits(n >> 2, ca, 0u), dna);
-                const float4 qb = chi2_1x4(g.bits(n >> 2, cb, 0u), dnb);
+                const float4 qa = chi2_1x4(g.bits(m, ca, 0u), dna);
+                const float4 qb = chi2_1x4(g.bits(m, cb, 0u), dnb);
                 const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
-#if PSS_PHASE_WALK
                 PhaseWalk w;
-                w.start(p, n);
-#endif
+                w.start(p, m);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
+                for (int e = 0; e < 4; ++e) {
                     uint32_t iv;
                     float u;
-#if PSS_PHASE_WALK
-                    if (i) w.step(dlo, dhi, M);
+                    if (e) w.step(dlo, dhi, M);
                     w.get_full(iv, u);       // fast_source(): nint == knot_m
-#else
-                    pchip_locate(k, (int64_t)(n + (uint32_t)i), iv, u);
-#endif
                     const float4 A = ptab[0][iv];
                     const float pa = fmaf(fmaf(fmaf(A.x, u, A.y), u, A.z), u, A.w);
                     float pb = pa;
@@ -1895,7 +1732,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                         const float4 Bc = ptab[1][iv];
                         pb = fmaf(fmaf(fmaf(Bc.x, u, Bc.y), u, Bc.z), u, Bc.w);
                     }
-                    lds[LdsC::at(b4 + i, n1)] = make_float2(pa * va[i], pb * vb[i]);
+                    lds[LdsC::at(b, n1 + e * NQ)] = make_float2(pa * va[e], pb * vb[e]);
                 }
             }
         } else
@@ -1904,34 +1741,10 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             const int b4 = (it - n1 * (B / 4)) * 4;
             const int64_t n = n1 * N2 + n20 + b4;
             float xa[4], xb[4], dum[4];
-            if constexpr (FAST && (kAbl & 1)) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) { xa[i] = (float)(n + i); xb[i] = (float)(n - i); }
-            } else if constexpr (FAST) {
-                const float4 qa = chi2_1x4(g.bits((uint32_t)(n >> 2), ca, (uint32_t)(n >> 34)));
-                const float4 qb = chi2_1x4(g.bits((uint32_t)(n >> 2), cb, (uint32_t)(n >> 34)));
-                const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    uint32_t iv;
-                    float u;
-                    pchip_locate(k, n + i, iv, u);
-                    if constexpr (kAbl & 16) {   // no profile-table gather
-                        xa[i] = hasa ? u * va[i] * p.draw_norm : 0.f;
-                        xb[i] = hasb ? (u + (float)iv) * vb[i] * p.draw_norm : 0.f;
-                    } else {
-                    xa[i] = hasa ? pchip_row(k, pra, iv, u) * va[i] * p.draw_norm : 0.f;
-                    xb[i] = hasb ? pchip_row(k, prb, iv, u) * vb[i] * p.draw_norm : 0.f;
-                    }
-                }
-            } else {
-            if (kAbl & 1) { for (int q = 0; q < 4; ++q) xa[q] = (float)(n + q); } else
             if (hasa) source4(k, ra, n, 4, xa, dum, true, false);
             else { xa[0] = xa[1] = xa[2] = xa[3] = 0.f; }
-            if (kAbl & 1) { for (int q = 0; q < 4; ++q) xb[q] = (float)(n - q); } else
             if (hasb) source4(k, rb, n, 4, xb, dum, true, false);
             else { xb[0] = xb[1] = xb[2] = xb[3] = 0.f; }
-            }
 #pragma unroll
             for (int i = 0; i < 4; ++i) lds[LdsC::at(b4 + i, n1)] = make_float2(xa[i], xb[i]);
         }
@@ -1951,7 +1764,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             cf *wl = lds + wv * LdsC::RS;
             FW::template load<RF0>(v, wl, lane);
             stage_sync<true>();
-            if constexpr (kMergeTw && !(kAbl & 6)) {
+            if constexpr (kMergeTw) {
                 // Last stage (radix RFL at Ns = N1/RFL) with the four-step
                 // twiddle folded in.  Output m of butterfly jj is k1 = jj +
                 // Ns m, and W_N^{n2 k1} = W_N^{n2 jj} W_N^{n2 Ns m}: the first
@@ -1979,7 +1792,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                     for (int m = 1; m < RFL; ++m) a[m] = cmul(a[m], U[m]);
                 }
             } else {
-                if constexpr (!(kAbl & 2)) FW::template run_tw<false, 1, F...>(v, wl, lane, tw16);
+                FW::template run_tw<false, 1, F...>(v, wl, lane, tw16);
 #pragma unroll
                 for (int i = 0; i < E; ++i) {
                     int b0, k1;
@@ -1987,14 +1800,14 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                     const uint32_t m = (uint32_t)(n20 + wv) * (uint32_t)k1;
                     float rev = (float)m * invN;
                     if (rev >= 0.5f) rev -= 1.0f;
-                    if constexpr (!(kAbl & 4)) v[i] = cmul(v[i], expi_rev(-rev)); else v[i] = v[i];
+                    v[i] = cmul(v[i], expi_rev(-rev));
                 }
             }
             FW::template store<RFL>(v, wl, lane);
         } else {
             FF::template load<RF0>(v, lds, tid);
             __syncthreads();
-            if constexpr (!(kAbl & 2)) FF::template run_tw<false, 1, F...>(v, lds, tid, tw16);
+            FF::template run_tw<false, 1, F...>(v, lds, tid, tw16);
 #pragma unroll
             for (int i = 0; i < E; ++i) {
                 int b, k1;
@@ -2003,30 +1816,134 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                 const uint32_t m = (uint32_t)(n20 + b) * (uint32_t)k1;
                 float rev = (float)m * invN;
                 if (rev >= 0.5f) rev -= 1.0f;
-                if constexpr (!(kAbl & 4)) v[i] = cmul(v[i], expi_rev(-rev)); else v[i] = v[i];
+                v[i] = cmul(v[i], expi_rev(-rev));
             }
             FF::template store<RFL>(v, lds, tid);
         }
         __syncthreads();
-        cf *Y = k.Yd + (int64_t)pr * pstride(k);
-        const int64_t RP = rpitch(k);
-        if constexpr (kPairIL) {
-            // item = (row pair p, 4 columns): 4 x 16 B = (row k1, row N1 - k1)
-            // of 4 consecutive columns, contiguous
-            for (int it = tid; it < N1 / 2 * (B / 4); it += T) {
-                const int pp = it / (B / 4);
-                const int b4 = (it - pp * (B / 4)) * 4;
-                const int ka = il_row(pp, 0, N1), kb = il_row(pp, 1, N1);
-                PSS_DASSERT(((int64_t)pp * RP + n20 + b4 + 4) * 2 <= pstride(k));
-                float4 *dst = reinterpret_cast<float4 *>(Y + ((int64_t)pp * RP + n20 + b4) * 2);
+        spill_block(k, lds, tid, pr, n20);
+    }
+
+    // ------------------------------------------------------------------
+    // Wave-local fast pass A (the wave-column geometries: C3's 1024 x 4096
+    // and C5's 2048 x 8192 splits).  Wave wv owns column n2 = n20 + wv and
+    // lane l its rows l + 64 q (q < E) -- exactly the first Stockham stage's
+    // inputs -- and draws them itself: with pulse_draw's keying the Philox
+    // block m = (l + 64 q') N2 + n2 (q' < E/4) holds rows q' + (E/4) e, so the
+    // values go straight into the registers (no LDS staging, no transpose and
+    // no workgroup barrier before the FFT); the phases walk the column in
+    // strides of 64 N2 samples.  Bitwise the values of passA<true>.
+    // ------------------------------------------------------------------
+    static constexpr bool kWaveA = kWaveCols && kMergeTw && kItemsExact && RF0 == 16 && (N1 % 64 == 0);
+    template <bool SHARED>
+    __device__ static void passA_wave(const KP &k) {
+        static_assert(kWaveA, "wave-local pass A: one wave per column");
+        __shared__ __align__(128) cf lds[B * LdsC::RS];   // (128-B aligned: the FFT's byte-address exchanges)
+        __shared__ cf tw16[kTw16Size];
+        __shared__ float4 ptab[SHARED ? 1 : 2][kFastNint];
+        const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+        tw16_fill(tw16, tid, T);
+        int cbx, pr;
+        xcd_block(cbx, pr);
+        const int ra = 2 * pr - k.poff, rb = ra + 1;
+        const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
+        const int64_t n20 = (int64_t)cbx * B;
+        const int64_t N2 = k.N2;
+        const PssPipeline &p = k.p;
+        const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
+        const int pra = (p.prof_rows == 1) ? 0 : (int)ca - p.prof_row0, prb = (p.prof_rows == 1) ? 0 : (int)cb - p.prof_row0;
+        const Rng g(p.seed, p.call_gen, P_PULSE);
+        {
+            const int nint = p.nint, last = p.prof_rows - 1;
+            const int rowa = min(max(pra, 0), last), rowb = min(max(prb, 0), last);
+            const float4 *prof = reinterpret_cast<const float4 *>(p.prof);
+            for (int i = tid; i < nint; i += T) {
+                ptab[0][i] = prof[(int64_t)rowa * nint + i];
+                if constexpr (!SHARED) ptab[SHARED ? 0 : 1][i] = prof[(int64_t)rowb * nint + i];
+            }
+        }
+        __syncthreads();                // the tables (tw16 is first read in the FFT's second stage)
+        const float dna = hasa ? p.draw_norm : 0.f, dnb = hasb ? p.draw_norm : 0.f;
+        const uint32_t n2 = (uint32_t)(n20 + wv);
+        cf v[E];
+        {
+            // register ib R0 + q holds row lane + 64 ib + LR q (the first
+            // stage's input mapping, Fft::load); a Philox block covers rows
+            // r + e N1/4 = registers + 4 e (R0 = 16: N1/4 = 4 LR)
+            static_assert(RF0 == 16, "wave-local pass A: radix-16 first stage");
+            constexpr int LR = N1 / RF0;
+            uint32_t dlo;
+            uint64_t dhi;
+            phase_delta_n(p, (uint64_t)LR * (uint64_t)N2, dlo, dhi);
+            const uint32_t M = p.knot_m;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const cf a = lds[LdsC::at(b4 + i, ka)], b = lds[LdsC::at(b4 + i, kb)];
-                    dst[i] = make_float4(a.x, a.y, b.x, b.y);
+            for (int ib = 0; ib < E / RF0; ++ib) {
+                // profile values of the rows, in the register of their row
+                PhaseWalk w;
+                w.start(p, (uint32_t)(lane + 64 * ib) * (uint32_t)N2 + n2);   // N <= 2^24
+#pragma unroll
+                for (int q = 0; q < RF0; ++q) {
+                    uint32_t iv;
+                    float u;
+                    if (q) w.step(dlo, dhi, M);
+                    w.get_full(iv, u);       // fast_source(): nint == knot_m
+                    const float4 A = ptab[0][iv];
+                    const float pa = fmaf(fmaf(fmaf(A.x, u, A.y), u, A.z), u, A.w);
+                    float pb = pa;
+                    if constexpr (!SHARED) {
+                        const float4 Bc = ptab[SHARED ? 0 : 1][iv];
+                        pb = fmaf(fmaf(fmaf(Bc.x, u, Bc.y), u, Bc.z), u, Bc.w);
+                    }
+                    v[ib * RF0 + q] = make_float2(pa, pb);
+                }
+                // times the draws: block of row lane + 64 ib + LR q (q < 4)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t m = (uint32_t)(lane + 64 * ib + LR * q) * (uint32_t)N2 + n2;
+                    const float4 qa = chi2_1x4(g.bits(m, ca, 0u), dna);
+                    const float4 qb = chi2_1x4(g.bits(m, cb, 0u), dnb);
+                    const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        cf &x = v[ib * RF0 + q + 4 * e];
+                        x = make_float2(x.x * va[e], x.y * vb[e]);
+                    }
                 }
             }
-            return;
         }
+        // column FFT (wave-local) with the four-step twiddle merged into the
+        // last stage: as passA
+        cf *wl = lds + wv * LdsC::RS;
+        FW::template run_head_tw<false, 1, F...>(v, wl, lane, tw16);
+        {
+            constexpr int NsL = N1 / RFL;
+            constexpr int LG1 = __builtin_ctz((unsigned)N1);
+            const int LGN = __builtin_ctzll((unsigned long long)k.N);        // N = 2^LGN here
+            const uint32_t A = n2 << (32 - LGN);                              // n2 / N (2^-32 rev)
+            cf U[RFL];
+#pragma unroll
+            for (int m = 1; m < RFL; ++m) U[m] = expi_rev(-fix32_to_rev(A * (uint32_t)(NsL * m)));
+#pragma unroll
+            for (int ib = 0; ib < E / RFL; ++ib) {
+                const uint32_t jj = (uint32_t)(lane + 64 * ib);              // < NsL
+                const uint32_t X0 = jj * A, S = jj << (32 - LG1);
+                cf *a = v + ib * RFL;
+#pragma unroll
+                for (int q = 0; q < RFL; ++q) a[q] = cmul(a[q], expi_rev(-fix32_to_rev(X0 + (uint32_t)q * S)));
+                dft<RFL, false>(a);
+#pragma unroll
+                for (int m = 1; m < RFL; ++m) a[m] = cmul(a[m], U[m]);
+            }
+        }
+        FW::template store<RFL>(v, wl, lane);
+        __syncthreads();
+        spill_block(k, lds, tid, pr, n20);
+    }
+    // The spill of a column block from LDS (natural k1 per column row):
+    // 16-B stores of 4 columns per row k1, 32 consecutive rows per 32-lane group.
+    __device__ static __forceinline__ void spill_block(const KP &k, const cf *lds, int tid, int pr, int64_t n20) {
+        cf *Y = k.Yd + (int64_t)pr * pstride(k);
+        const int64_t RP = rpitch(k);
         for (int it = tid; it < N1 * B / 4; it += T) {
             int k1, b4;
             if constexpr (B < 32 && N1 % 32 == 0) {
@@ -2044,15 +1961,8 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             cf a2 = lds[LdsC::at(b4 + 2, k1)], a3 = lds[LdsC::at(b4 + 3, k1)];
             PSS_DASSERT((int64_t)k1 * RP + n20 + b4 + 4 <= pstride(k));
             float4 *dst = reinterpret_cast<float4 *>(Y + (int64_t)k1 * RP + n20 + b4);
-            if constexpr (PSS_SPILL_NT) {
-                typedef float v4f __attribute__((ext_vector_type(4)));
-                v4f *d4 = reinterpret_cast<v4f *>(dst);
-                __builtin_nontemporal_store((v4f){a0.x, a0.y, a1.x, a1.y}, d4);
-                __builtin_nontemporal_store((v4f){a2.x, a2.y, a3.x, a3.y}, d4 + 1);
-            } else {
-                dst[0] = make_float4(a0.x, a0.y, a1.x, a1.y);
-                dst[1] = make_float4(a2.x, a2.y, a3.x, a3.y);
-            }
+            dst[0] = make_float4(a0.x, a0.y, a1.x, a1.y);
+            dst[1] = make_float4(a2.x, a2.y, a3.x, a3.y);
         }
     }
 
@@ -2193,45 +2103,13 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         const Buf Y(Yp, (uint32_t)(pstride(k) * 8));   // one pair spill, < 2^28 bytes
         const uint32_t RP = (uint32_t)rpitch(k);
         const uint32_t s0 = (uint32_t)n20 * 8u;        // wave-uniform part of the offset
-        if constexpr (kPairIL) {
-#pragma unroll 1
-            for (int it = tid; it < N1 / 2 * (B / 4); it += T) {
-                const int pp = it / (B / 4);
-                const int b4 = (it - pp * (B / 4)) * 4;
-                const uint32_t off = ((uint32_t)pp * RP + (uint32_t)b4) * 16u;
-                float4 q[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) q[i] = Y.ld4<PSS_SPILL_AUX>(off + 16u * i, 2u * s0);
-#pragma unroll
-                for (int side = 0; side < 2; ++side) {
-                    const int k1 = il_row(pp, side, N1);
-                    const uint32_t m0 = (uint32_t)(n20 + b4) * (uint32_t)k1;
-                    float r0 = (float)m0 * invN;
-                    if (r0 >= 0.5f) r0 -= 1.0f;
-                    float r1 = (float)k1 * invN;
-                    if (r1 >= 0.5f) r1 -= 1.0f;
-                    const cf w0 = expi_rev(r0), w1 = expi_rev(r1);
-                    const cf w2 = cmul(w1, w1);
-                    const cf tw[4] = {w0, cmul(w0, w1), cmul(w0, w2), cmul(w0, cmul(w2, w1))};
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const cf a = side ? make_float2(q[i].z, q[i].w) : make_float2(q[i].x, q[i].y);
-                        if constexpr (!(kAbl & 4)) lds[LdsC::at(b4 + i, k1)] = cmul(a, tw[i]); else lds[LdsC::at(b4 + i, k1)] = a;
-                    }
-                }
-            }
-        } else {
+        {
 #pragma unroll 1
         for (int it = tid; it < N1 * B / 4; it += T) {
             const int k1 = it / (B / 4);
             const int b4 = (it - k1 * (B / 4)) * 4;
-            uint32_t off = ((uint32_t)k1 * RP + (uint32_t)b4) * 8u;
-            uint32_t so = s0;
-            if constexpr (kAbl & 128) {   // ablation: contiguous loads (wrong data)
-                off = (uint32_t)it * 32u;
-                so = (uint32_t)n20 * (uint32_t)(N1 * 8);
-            }
-            const float4 lo = Y.ld4<PSS_SPILL_AUX>(off, so), hi = Y.ld4<PSS_SPILL_AUX>(off + 16u, so);
+            const uint32_t off = ((uint32_t)k1 * RP + (uint32_t)b4) * 8u;
+            const float4 lo = Y.ld4(off, s0), hi = Y.ld4(off + 16u, s0);
             const cf a[4] = {make_float2(lo.x, lo.y), make_float2(lo.z, lo.w),
                              make_float2(hi.x, hi.y), make_float2(hi.z, hi.w)};
             // W^{m}, m = (n20 + b4 + i) k1 < N (exact in 32-bit and float):
@@ -2246,7 +2124,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             const cf tw[4] = {w0, cmul(w0, w1), cmul(w0, w2), cmul(w0, cmul(w2, w1))};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                if constexpr (!(kAbl & 4)) lds[LdsC::at(b4 + i, k1)] = cmul(a[i], tw[i]); else lds[LdsC::at(b4 + i, k1)] = a[i];
+                lds[LdsC::at(b4 + i, k1)] = cmul(a[i], tw[i]);
             }
         }
         }
@@ -2257,12 +2135,12 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             cf *wl = lds + wv * LdsC::RS;
             FW::template load<RI0>(v, wl, lane);
             stage_sync<true>();
-            if constexpr (!(kAbl & 2)) FW::template run_tw<true, 1, I...>(v, wl, lane, tw16);
+            FW::template run_tw<true, 1, I...>(v, wl, lane, tw16);
             FW::template store<RIL>(v, wl, lane);
         } else {
             FF::template load<RI0>(v, lds, tid);
             __syncthreads();
-            if constexpr (!(kAbl & 2)) FF::template run_tw<true, 1, I...>(v, lds, tid, tw16);
+            FF::template run_tw<true, 1, I...>(v, lds, tid, tw16);
             FF::template store<RIL>(v, lds, tid);
         }
         __syncthreads();
@@ -2305,29 +2183,22 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                 ma[i] = ((ha >> i) & 1u) ? 2.0f : 0.0f;
                 mb[i] = ((hb >> i) & 1u) ? 2.0f : 0.0f;
             }
-            if (kAbl & 1) { *reinterpret_cast<float4 *>(k.p.data + (int64_t)ra * k.p.ld + n) = make_float4(da[0] + ma[0], da[1], da[2], da[3]); *reinterpret_cast<float4 *>(k.p.data + (int64_t)rb * k.p.ld + n) = make_float4(db[0] + mb[0], db[1], db[2], db[3]); continue; }
             if (hasa) epilogue4(k, ra, n, 4, da, ma, false);
             if (hasb) epilogue4(k, rb, n, 4, db, mb, false);
         }
     }
 
-    // C, fast path (host-selected: Philox draws with df = 1 for noise and
-    // null replacement, no injected draws, no observe() copy).  Bitwise equal
-    // to passC.  Every sample is stored as signal + noise, or, at the
-    // positions a delayed null's mask table marks for its channel (PSS_FUSE_NULL),
-    // as replacement + noise; with PSS_FUSE_NULL=0 those are rewritten
-    // afterwards by k_null_fix_list instead.
-    // NBLK adjacent column blocks per workgroup, one after the other through
-    // the same LDS, their outputs held in registers and stored together: the
-    // two 64-B halves of every 128-B output line (16 columns x 4 B per
-    // channel row) leave the same lane in back-to-back stores instead of from
-    // two workgroups (whose halves do not always meet in L2: PMC writes were
-    // 1.11x the algorithmic bytes with NBLK = 1).
-    // C, fast path with 32-column blocks (PSS_PC32; N1 = 1024, T = 1024):
-    // 128-B output segments per channel row instead of 64 (tools/seg_bw.hip:
-    // 64-B write segments run at 5.2 TB/s against 6.6 for 128 B).  32 columns
-    // of 1024 rows are 256 KB, so they cannot all sit in LDS: each wave keeps
-    // its two columns (w, w + 16) in registers between three LDS phases --
+    // C, fast path (host-selected: Philox draws with df = 1 for the noise, no
+    // injected draws, no observe() copy).  Bitwise equal to passC: every
+    // sample is stored as signal + noise; a delayed null's samples are
+    // rewritten afterwards by k_null_fix_list (fusing the table lookups here
+    // measured 27.0 ms against 16.6 + 2.5 for pass C + fix-up, round 2).
+    // C, fast path with register-resident columns (C5's 2048-point columns,
+    // 16 columns per 512-thread workgroup: 64-B output segments per channel
+    // row instead of 32; tools/seg_bw.hip: 64-B write segments run at 5.2
+    // TB/s against 3.1 for 32 B).  16 columns of 2048 rows are 256 KB, so
+    // they cannot all sit in LDS: each wave keeps its columns in registers
+    // between three LDS phases --
     // (1) the spill rows in two halves of 512 (256-B row segments, twiddled as
     // in inv_block) staged in LDS and picked up into the FFT input mapping,
     // (2) the two wave-local inverse FFTs one after the other through the
@@ -2407,7 +2278,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
 #pragma unroll
             for (int c = 0; c < CPW; ++c) {
                 if (c) stage_sync<true>();
-                if constexpr (!(kAbl & 2)) FWC::template run_tw<true, 1, I...>(v[c], wl, lane, tw16);
+                FWC::template run_tw<true, 1, I...>(v[c], wl, lane, tw16);
             }
         }
         // (3) per channel: stage the scaled outputs, store rows with the noise
@@ -2444,13 +2315,12 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         }
     }
 
-    template <int NBLK = 1>
     __device__ static void passC_fast(const KP &k) {
         static_assert(kItemsExact, "fast pass C: whole items per thread");
         __shared__ __align__(128) cf lds[B * LdsC::RS];
         const int tid = threadIdx.x;
-        int cbx2, pr;
-        xcd_block(cbx2, pr);
+        int cbx, pr;
+        xcd_block(cbx, pr);
         const int ra = 2 * pr - k.poff, rb = ra + 1;
         const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
         const int64_t N2 = k.N2;
@@ -2458,92 +2328,36 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         const float invN = k.invN, nn = p.noise_norm;
         const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
         const Rng gn(p.seed, p.call_noise, P_NOISE);
-        // fused delayed null (kFuseNull): the channels' table splits
-        const bool mnull = kFuseNull && k.mtab;
-        uint32_t isa = 0, isb = 0;
-        float tma = 0.f, tmb = 0.f;
-        if (mnull) {
-            if (hasa) mask_split((uint64_t)p.mask_ramp[ra], k.log2n, isa, tma);
-            if (hasb) mask_split((uint64_t)p.mask_ramp[rb], k.log2n, isb, tmb);
-        }
-        const Rng gr(p.seed, p.call_null, P_REP);
-        const float sc = p.null_rep_scale;
         const uint32_t rbytes = (uint32_t)(k.N * 4);
         const Buf oa(p.data + (int64_t)max(ra, 0) * p.ld, rbytes), ob(p.data + (int64_t)min(rb, p.nchan - 1) * p.ld, rbytes);
-        float acc[NBLK][ITEMS][2][4];
-#pragma unroll
-        for (int blk = 0; blk < NBLK; ++blk) {
-            const int64_t n20 = (int64_t)(cbx2 * NBLK + blk) * B;
-            if (blk) __syncthreads();            // the previous block's epilogue has read LDS
-            inv_block(k, k.Yd + (int64_t)pr * pstride(k), n20, lds, tid);
-#pragma unroll
-            for (int t = 0; t < ITEMS; ++t) {
-                const int it = tid + t * T;
-                const int n1 = it / (B / 4);
-                const int b4 = (it - n1 * (B / 4)) * 4;
-                const uint32_t n = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4;   // N <= 2^24
-                float4 xa, xb;
-                if constexpr (kAbl & 1) {
-                    const float fn = (float)n;
-                    xa = make_float4(fn, fn + 1.f, fn + 2.f, fn + 3.f);
-                    xb = make_float4(fn, fn - 1.f, fn - 2.f, fn - 3.f);
-                } else {
-                    xa = chi2_1x4(gn.bits(n >> 2, ca, 0u));
-                    xb = chi2_1x4(gn.bits(n >> 2, cb, 0u));
-                }
-                const float na[4] = {xa.x, xa.y, xa.z, xa.w}, nb[4] = {xb.x, xb.y, xb.z, xb.w};
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const cf z = lds[LdsC::at(b4 + i, n1)];
-                    acc[blk][t][0][i] = fmaf(nn, na[i], z.x * invN);
-                    acc[blk][t][1][i] = fmaf(nn, nb[i], z.y * invN);
-                }
-                if (mnull) {
-                    // nulled samples: replacement + noise, the draws and
-                    // expression of epilogue4 / k_null_fix_list (bitwise equal)
-                    const uint32_t ha = hasa ? mask_hits4(k, (int64_t)n, isa, tma) : 0u;
-                    const uint32_t hb = hasb ? mask_hits4(k, (int64_t)n, isb, tmb) : 0u;
-                    if (ha) {
-                        const float4 r = chi2_1x4(gr.bits(n >> 2, ca, 0u));
-                        const float vr[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            if ((ha >> i) & 1u) acc[blk][t][0][i] = fmaf(nn, na[i], vr[i] * sc);
-                    }
-                    if (hb) {
-                        const float4 r = chi2_1x4(gr.bits(n >> 2, cb, 0u));
-                        const float vr[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            if ((hb >> i) & 1u) acc[blk][t][1][i] = fmaf(nn, nb[i], vr[i] * sc);
-                    }
-                }
-            }
-        }
+        const int64_t n20 = (int64_t)cbx * B;
+        inv_block(k, k.Yd + (int64_t)pr * pstride(k), n20, lds, tid);
+        float acc[ITEMS][2][4];
 #pragma unroll
         for (int t = 0; t < ITEMS; ++t) {
             const int it = tid + t * T;
             const int n1 = it / (B / 4);
             const int b4 = (it - n1 * (B / 4)) * 4;
+            const uint32_t n = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4;   // N <= 2^24
+            const float4 xa = chi2_1x4(gn.bits(n >> 2, ca, 0u));
+            const float4 xb = chi2_1x4(gn.bits(n >> 2, cb, 0u));
+            const float na[4] = {xa.x, xa.y, xa.z, xa.w}, nb[4] = {xb.x, xb.y, xb.z, xb.w};
 #pragma unroll
-            for (int blk = 0; blk < NBLK; ++blk) {
-                const int64_t n20 = (int64_t)(cbx2 * NBLK + blk) * B;
-                const uint32_t off = ((uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4) * 4u;
-                if constexpr (kAbl & 64) {   // ablation: contiguous stores (wrong place)
-                    const uint32_t o2 = ((uint32_t)((cbx2 * NBLK + blk) * T * ITEMS) + (uint32_t)it) * 16u;
-                    if (hasa) oa.st4(acc[blk][t][0][0], acc[blk][t][0][1], acc[blk][t][0][2], acc[blk][t][0][3], o2, 0);
-                    if (hasb) ob.st4(acc[blk][t][1][0], acc[blk][t][1][1], acc[blk][t][1][2], acc[blk][t][1][3], o2, 0);
-                    continue;
-                }
-                if (hasa) oa.st4<PSS_OUT_AUX>(acc[blk][t][0][0], acc[blk][t][0][1], acc[blk][t][0][2], acc[blk][t][0][3], off, 0);
+            for (int i = 0; i < 4; ++i) {
+                const cf z = lds[LdsC::at(b4 + i, n1)];
+                acc[t][0][i] = fmaf(nn, na[i], z.x * invN);
+                acc[t][1][i] = fmaf(nn, nb[i], z.y * invN);
             }
+        }
+        // (a delayed null's samples are rewritten afterwards: k_null_fix_list)
 #pragma unroll
-            for (int blk = 0; blk < NBLK; ++blk) {
-                if constexpr (kAbl & 64) continue;
-                const int64_t n20 = (int64_t)(cbx2 * NBLK + blk) * B;
-                const uint32_t off = ((uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4) * 4u;
-                if (hasb) ob.st4<PSS_OUT_AUX>(acc[blk][t][1][0], acc[blk][t][1][1], acc[blk][t][1][2], acc[blk][t][1][3], off, 0);
-            }
+        for (int t = 0; t < ITEMS; ++t) {
+            const int it = tid + t * T;
+            const int n1 = it / (B / 4);
+            const int b4 = (it - n1 * (B / 4)) * 4;
+            const uint32_t off = ((uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4) * 4u;
+            if (hasa) oa.st4(acc[t][0][0], acc[t][0][1], acc[t][0][2], acc[t][0][3], off, 0);
+            if (hasb) ob.st4(acc[t][1][0], acc[t][1][1], acc[t][1][2], acc[t][1][3], off, 0);
         }
     }
 
@@ -2579,10 +2393,12 @@ template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairA(KP k) { C::template passA<false>(k); }
 template <typename C, int T, bool SHARED>
 __global__ __launch_bounds__(T) void k_pairA_fast(KP k) { C::template passA<true, SHARED>(k); }
+template <typename C, int T, bool SHARED>
+__global__ __launch_bounds__(T) void k_pairA_wave(KP k) { C::template passA_wave<SHARED>(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairC(KP k) { C::passC(k); }
-template <typename C, int T, int NBLK>
-__global__ __launch_bounds__(T) void k_pairC_fast(KP k) { C::template passC_fast<NBLK>(k); }
+template <typename C, int T>
+__global__ __launch_bounds__(T) void k_pairC_fast(KP k) { C::passC_fast(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T, T == 512 ? 2 : 4) void k_pairC_fast32(KP k) { C::passC_fast32(k); }
 template <typename C, int T>
@@ -3147,7 +2963,13 @@ __global__ void k_chi2_fill(float *out, int64_t n, int32_t chan0, float df, uint
          it += (int64_t)gridDim.x * blockDim.x) {
         const int64_t n0 = it << 2;
         float x[4];
-        draw4(g, n0, (uint32_t)(chan0 + r), df, x);
+        if (purpose == P_PULSE && df == 1.0f && (n & 3) == 0) {
+            // the search pulses' layout (pulse_draw: rows of n samples)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = pulse_draw(g, n0 + i, n, (uint32_t)(chan0 + r), 1.0f);
+        } else {
+            draw4(g, n0, (uint32_t)(chan0 + r), df, x);
+        }
         for (int i = 0; i < 4 && n0 + i < n; ++i) out[(int64_t)r * n + n0 + i] = x[i];
     }
 }
@@ -3195,7 +3017,6 @@ using C1kI = RList<4, 16, 16>;
 using C2kF = RList<16, 16, 8>;
 using C2kI = RList<8, 16, 16>;
 using C4k = RList<16, 16, 16>;
-using C4k8 = RList<8, 8, 8, 8>;     // 4096 = 8^4: 8 values per thread at 1024 threads (PSS_ROW8)
 using C8kF = RList<16, 8, 8, 8>;
 using C8kI = RList<8, 8, 8, 16>;
 
@@ -3263,10 +3084,10 @@ static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
     WsLayout w;
     memset(&w, 0, sizeof(w));
     int64_t o = 0;
-    if (fourstep_len(N) && !filt) {
+    if (fourstep_len(N)) {
         const int64_t npairs = ((int64_t)nchan + 2) / 2;   // pairs of (even, odd) global channels
-        // pair spills: N1 <= N / 1024 rows of N2 + kSpillPad on every 2^m split
-        const int64_t ps = N + (N / 1024) * kSpillPad;
+        // pair spills: N1 x N2 complex per pair
+        const int64_t ps = N;
         w.yd = o;    o += al256(npairs * ps * 8);
         w.mspec = o; o += al256(N * 8);
         w.ynode = o; o += al256((int64_t)(KCH / 2) * ps * 8);
@@ -3295,7 +3116,7 @@ static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
             w.bs_bhat = o;  o += al256(g.M * 8);
             w.bs_z = o;     o += al256(g.nb * g.M * 8);
         }
-        if (smooth_split(N) && !filt) {
+        if (smooth_split(N)) {
             // mixed-radix four-step (inside the same bytes: the direct path
             // still serves these lengths for a delayed null)
             const int64_t npairs = ((int64_t)nchan + 2) / 2;
@@ -3436,31 +3257,6 @@ constexpr int xrs_read(int B) { return B >= 32 ? 1 : 16; }
 // gain nothing from the swizzle and the XOR addressing costs VALU)
 constexpr int xrs_write(int B) { return -1; }
 
-// Pair batches on two side streams (PSS_BATCHES > 1, fast path only): batch
-// b's pass A waits for batch b-1's pass A, so it runs next to batch b-1's
-// row pass (82 + 70 KB of LDS: both fit one CU) -- the compute-heavy
-// generator overlaps the memory-heavy passes instead of the three passes
-// running one after the other over all channels.  The batches are
-// independent pair ranges (per-row arrays offset, RNG keyed by global
-// channel): results are bitwise those of one launch.  Fork from / join to
-// the caller's stream with events, so the run stays stream-ordered.
-static int g_batches = -1;
-// PSS_BATCH_AFTER=row: batch b's pass A waits for batch b-1's ROW pass
-// instead, so it runs next to batch b-1's pass C (the VALU-bound generator
-// beside the memory-pattern-bound inverse columns; needs a pass C that leaves
-// LDS for a pass-A workgroup on the same CU, e.g. PSS_BC=8)
-static bool g_batch_after_row = false;
-static int batches_setting() {
-    if (g_batches < 0) {
-        const char *e = getenv("PSS_BATCHES");
-        const char *a = getenv("PSS_BATCH_AFTER");
-        g_batch_after_row = a && strcmp(a, "row") == 0;
-        g_batches = e ? atoi(e) : 1;
-        if (g_batches < 1) g_batches = 1;
-        if (g_batches > 16) g_batches = 16;
-    }
-    return g_batches;
-}
 struct SideStreams {
     hipStream_t s[2];
     hipEvent_t ev[40];
@@ -3485,45 +3281,6 @@ template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typena
           int TRF, int BC, int TC>
 static int launch_pair_passes(KP &k, hipStream_t st);
 
-template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typename RF, typename RI,
-          int TRF, int BC, int TC>
-static int launch_batches(KP &k, hipStream_t st, int nb) {
-    using PR = PairRows<N2, TR, RF, RI>;
-    SideStreams *ss = side_streams();
-    if (!ss) return fail(PSS_EHIP, "side streams");
-    hipEvent_t fork = ss->ev[0];
-    HIPCHK(hipEventRecord(fork, st));
-    for (int i = 0; i < 2; ++i) HIPCHK(hipStreamWaitEvent(ss->s[i], fork, 0));
-    for (int b = 0; b < nb; ++b) {
-        const int p0 = (int)((int64_t)b * k.npairs / nb), p1 = (int)((int64_t)(b + 1) * k.npairs / nb);
-        const int r0 = p0 == 0 ? 0 : 2 * p0 - k.poff;
-        const int r1 = min(2 * p1 - k.poff, k.p.nchan);
-        KP kb = k;
-        kb.poff = p0 == 0 ? k.poff : 0;
-        kb.npairs = p1 - p0;
-        kb.p.nchan = r1 - r0;
-        kb.p.chan0 = k.p.chan0 + r0;
-        kb.p.data = k.p.data + (int64_t)r0 * k.p.ld;
-        kb.p.ramp = k.p.ramp + r0;
-        kb.p.nyq_re = k.p.nyq_re + r0;
-        kb.p.nyq_im = k.p.nyq_im + r0;
-        if (k.p.mask_ramp) kb.p.mask_ramp = k.p.mask_ramp + r0;
-        kb.rtab = k.rtab + (int64_t)p0 * 2 * PR::RFL;
-        kb.Yd = k.Yd + (int64_t)p0 * pstride(k);
-        kb.after_a = ss->ev[1 + b];
-        hipStream_t sb = ss->s[b & 1];
-        if (b > 0) HIPCHK(hipStreamWaitEvent(sb, ss->ev[b], 0));     // batch b-1's pass A done
-        const int rc = launch_pair_passes<N1, B, T, CF, CI, N2, TR, RF, RI, TRF, BC, TC>(kb, sb);
-        if (rc) return rc;
-    }
-    for (int i = 0; i < 2; ++i) {
-        hipEvent_t j = ss->ev[20 + i];
-        HIPCHK(hipEventRecord(j, ss->s[i]));
-        HIPCHK(hipStreamWaitEvent(st, j, 0));
-    }
-    return PSS_OK;
-}
-
 // BC/TC: column-block width and threads of the FAST pass C (the spill layout
 // does not depend on the block width, so pass C may use wider blocks than pass
 // A: its output rows are written in BC-sample (4 BC-byte) segments).
@@ -3538,7 +3295,6 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
     char *w = reinterpret_cast<char *>(k.p.work);
     const WsLayout L = ws_layout(k.p.nchan, k.N);
     k.Yd = reinterpret_cast<cf *>(w + L.yd);
-    k.sp = ((N1 & (N1 - 1)) == 0) ? N2 + kSpillPad : N2;   // (ws_layout sizes the pad for 2^m)
     if (k.p.null_mode == PSS_NULL_DELAYED) {
         // the mask table's position arithmetic is for N = 2^m (validate()
         // sends delayed nulls of other lengths to the direct path)
@@ -3547,7 +3303,7 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
             // table before the null fix-up: build it on a side stream next to
             // pass A (its dozen small launches then cost no time on the main
             // stream); the fix-up waits for it.
-            SideStreams *ss = (PSS_MASK_SIDE && k.p.data_in_fft && g_batches <= 1) ? side_streams() : nullptr;
+            SideStreams *ss = k.p.data_in_fft ? side_streams() : nullptr;
             hipStream_t ms = st;
             if (ss) {
                 HIPCHK(hipEventRecord(ss->ev[30], st));
@@ -3573,16 +3329,13 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
         LAUNCHCHK();
         return PSS_OK;
     }
-    {
+    if (!k.p.htab) {   // (a transfer-function run has no ramps)
         cf *rt = reinterpret_cast<cf *>(w + L.rtab);
         k_pair_tab<PR::RFL><<<dim3((unsigned)k.npairs), dim3(64), 0, st>>>(k.p.ramp, k.N, k.p.nchan, k.poff,
                                                                           k.npairs, rt);
         LAUNCHCHK();
         k.rtab = rt;
     }
-    const bool fast = PCC::kItemsExact && fast_epilogue(k);
-    const int nb = (fast && fast_source(k.p) && g_batches > 1 && k.npairs >= 4 * g_batches) ? g_batches : 1;
-    if (nb > 1) return launch_batches<N1, B, T, CF, CI, N2, TR, RF, RI, TRF, BC, TC>(k, st, nb);
     return launch_pair_passes<N1, B, T, CF, CI, N2, TR, RF, RI, TRF, BC, TC>(k, st);
 }
 
@@ -3605,8 +3358,13 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     if (launched) {
     } else if constexpr (PC::kItemsExact) {
         if (fast_source(k.p)) {
-            if (k.p.prof_rows == 1) k_pairA_fast<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
-            else k_pairA_fast<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
+            if constexpr (PC::kWaveA) {
+                if (k.p.prof_rows == 1) k_pairA_wave<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
+                else k_pairA_wave<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
+            } else {
+                if (k.p.prof_rows == 1) k_pairA_fast<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
+                else k_pairA_fast<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
+            }
         } else {
             k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
         }
@@ -3615,11 +3373,12 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     }
     tk_end(st);
     LAUNCHCHK();
-    if (k.after_a && !g_batch_after_row) HIPCHK(hipEventRecord(k.after_a, st));   // batching: the next batch's pass A may start
     tk_begin(TK_ROW, st);
-    if (k.p.tail_a) {
+    if (k.p.htab) {
+        k_pair_row<PR, TR, false, true><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
+    } else if (k.p.tail_a) {
         k_pair_row<PR, TR, true><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
-    } else if constexpr (PSS_ROW_SEQ && (N2 == 8192 || (PSS_ROW_SEQ4K && N2 == 4096))) {
+    } else if constexpr (N2 == 8192) {
         constexpr int TS = N2 / 16;                  // 16 values of each row per thread
         using PRS = PairRowsSeq<N2, TS, RF, RI>;
         k_pair_row_seq<PRS, TS, false><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2 - 1)), dim3(TS), 0, st>>>(k);
@@ -3629,27 +3388,17 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     }
     tk_end(st);
     LAUNCHCHK();
-    if (k.after_a && g_batch_after_row) HIPCHK(hipEventRecord(k.after_a, st));
     const bool fast = PCC::kItemsExact && fast_epilogue(k);
-    // the generic pass C reads the bits, the fused fast one the table
-    if (k.mask_ready && (!fast || kFuseNull)) HIPCHK(hipStreamWaitEvent(st, k.mask_ready, 0));
+    // the generic pass C reads the null decisions as bits
+    if (k.mask_ready && !fast) HIPCHK(hipStreamWaitEvent(st, k.mask_ready, 0));
     tk_begin(TK_COLC, st);
     if (fast) {
-        if constexpr (PCC::kItemsExact)
-        {
-            // PSS_PC_NBLK = 2: two adjacent column blocks per workgroup
-            // (rejected from the ISA, not run: block 0's 32 output registers stay live
-            // through block 1 and the kernel spills 31 VGPRs at the 128 cap)
-            if constexpr (PSS_C5_WIDE && N1 == 2048 && N2 % 16 == 0)
+        if constexpr (PCC::kItemsExact) {
+            if constexpr (N1 == 2048 && N2 % 16 == 0)
                 k_pairC_fast32<PairCols<N1, 16, 512, CF, CI, -1>, 512>
                     <<<dim3((unsigned)(N2 / 16), (unsigned)k.npairs), dim3(512), 0, st>>>(k);
-            else if constexpr (PSS_PC32 && N1 == 1024 && N2 % 32 == 0 && TC == 1024)
-                k_pairC_fast32<PairCols<N1, 32, PSS_PC32_T, CF, CI, -1>, PSS_PC32_T>
-                    <<<dim3((unsigned)(N2 / 32), (unsigned)k.npairs), dim3(PSS_PC32_T), 0, st>>>(k);
-            else if constexpr (PSS_PC_NBLK == 2 && (N2 / BC) % 2 == 0)
-                k_pairC_fast<PCC, TC, 2><<<dim3((unsigned)(N2 / BC / 2), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
             else
-                k_pairC_fast<PCC, TC, 1><<<dim3((unsigned)(N2 / BC), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
+                k_pairC_fast<PCC, TC><<<dim3((unsigned)(N2 / BC), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
         }
     } else if (PC::kRegCols && fold_epilogue(k)) {
         if constexpr (PC::kRegCols) {
@@ -3664,16 +3413,12 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     }
     tk_end(st);
     LAUNCHCHK();
-    if (fast && k.mtab && !kFuseNull) {
+    if (fast && k.mtab) {
         if (k.mask_ready) HIPCHK(hipStreamWaitEvent(st, k.mask_ready, 0));
         tk_begin(TK_NULLFIX, st);
-        if (PSS_NULL_LIST) {
-            // grid-stride over the word list: ~1/8 of the words per channel
-            const unsigned gx = (unsigned)((k.N / 32 / 8 + 255) / 256);
-            k_null_fix_list<<<dim3(gx ? gx : 1, (unsigned)k.p.nchan), dim3(256), 0, st>>>(k);
-        } else {
-            k_null_fix<<<dim3((unsigned)((k.N / 32 + 255) / 256), (unsigned)k.p.nchan), dim3(256), 0, st>>>(k);
-        }
+        // grid-stride over the word list: ~1/8 of the words per channel
+        const unsigned gx = (unsigned)((k.N / 32 / 8 + 255) / 256);
+        k_null_fix_list<<<dim3(gx ? gx : 1, (unsigned)k.p.nchan), dim3(256), 0, st>>>(k);
         tk_end(st);
         LAUNCHCHK();
     }
@@ -3682,40 +3427,30 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
 
 static int run_fourstep(KP &k, hipStream_t st, const float *mask_row) {
     const int64_t N = k.N;
-    if (kSplit4k && N == (1 << 22)) {
+    if (N == (1 << 22)) {
+        // C3: 1024 x 4096 (two 4096-point rows of a pair in 66 KB: two row
+        // workgroups per CU; 16-column pass-C blocks, 64-B output segments)
         k.N2 = 4096;
         k.N1 = 1024;
-        if constexpr (PSS_ROW8)
-            return launch_pair<1024, 8, 512, C1kF, C1kF, 4096, 1024, C4k8, C4k8, 256, PSS_BC, PSS_TC>(k, st, mask_row);
-        else
-            return launch_pair<1024, 8, 512, C1kF, C1kF, 4096, 512, C4k, C4k, 256, PSS_BC, PSS_TC>(k, st, mask_row);
+        return launch_pair<1024, 8, 512, C1kF, C1kF, 4096, 512, C4k, C4k, 256, kBC, kTC>(k, st, mask_row);
     }
-    if (N == (1 << 22)) {
-        // 512 x 8192 split (layout experiment; the 1024 x 4096 split above is
-        // the product default)
+    if (N == (1 << 23)) {
         k.N2 = 8192;
-        k.N1 = 512;
-        return launch_pair<512, 16, 512, C512F, C512F, 8192, 1024, C8kF, C8kI, 512, PSS_BC8, PSS_TC8>(k, st, mask_row);
+        k.N1 = 1024;
+        return launch_pair<1024, 8, 512, C1kF, C1kF, 8192, 1024, C8kF, C8kI, 512>(k, st, mask_row);
     }
     if (N == (1 << 24)) {
-        // C5 rows: 2048 x 8192; the fast pass C takes 8 columns per workgroup
-        // (1024 threads, 139 KB LDS) for 32-B output segments instead of 16
+        // C5 rows: 2048 x 8192.  Pass A: 8 columns, one wave per 2048-point
+        // column (wave-local FFTs, 32 values per lane; 64-B spill segments);
+        // pass C: 16-column register-resident blocks (passC_fast32)
         k.N2 = 8192;
         k.N1 = 2048;
-        // pass A: 8 columns, one wave per 2048-point column (wave-local FFTs,
-        // 32 values per lane; 64-B spill segments): 40.5 -> 33.3 ms against
-        // the 4-column workgroup-FFT kernel (profiles/r03/s14, one box).  The
-        // same for pass C (PSS_C5_WAVE) measured 44.5-44.9 -> 47.8-48.0: pass
-        // C keeps 1024 threads on its 8 columns.
-        if constexpr (PSS_C5_WAVE)
-            return launch_pair<2048, 8, 512, C2kF, C2kF, 8192, 1024, C8kF, C8kI, 512, 8, 512>(k, st, mask_row);
-        else
-            return launch_pair<2048, 8, 512, C2kF, C2kF, 8192, 1024, C8kF, C8kI, 512, 8, 1024>(k, st, mask_row);
+        return launch_pair<2048, 8, 512, C2kF, C2kF, 8192, 1024, C8kF, C8kI, 512, 8, 1024>(k, st, mask_row);
     }
-    if (PSS_ROW4K && N >= (1 << 17) && N <= (1 << 21)) {
-        // rows of 4096 (the C3 row kernel: two rows of a pair in 66 KB, two
-        // workgroups per CU) and N / 4096 columns; the column kernels keep
-        // their 8192 / N1-column blocks (N2 / B >= 16 blocks per pair)
+    if (N >= (1 << 17)) {
+        // 2^17 .. 2^21: rows of 4096 (the C3 row kernel: two rows of a pair
+        // in 66 KB, two workgroups per CU) and N / 4096 columns; the column
+        // kernels keep their 8192 / N1-column blocks (N2 / B >= 16 per pair)
         k.N2 = 4096;
         k.N1 = N / 4096;
         switch (k.N1) {
@@ -3731,26 +3466,6 @@ static int run_fourstep(KP &k, hipStream_t st, const float *mask_row) {
             default: break;
         }
         return fail(PSS_EUNSUPPORTED, "four-step: N=%lld", (long long)N);
-    }
-    if (N >= (1 << 17)) {
-        k.N2 = 8192;
-        k.N1 = N / 8192;
-        switch (k.N1) {
-#define CASE8K(N1_, CF, CI)                                                                          \
-    case N1_:                                                                                        \
-        return launch_pair<N1_, 8192 / N1_, 512, CF, CF, 8192, 1024, C8kF, C8kI, 512>(k, st, mask_row);
-            CASE8K(16, C16, C16)
-            CASE8K(32, C32F, C32I)
-            CASE8K(64, C64F, C64I)
-            CASE8K(128, C128F, C128I)
-            CASE8K(256, C256, C256)
-            CASE8K(512, C512F, C512I)
-            CASE8K(1024, C1kF, C1kI)
-            CASE8K(2048, C2kF, C2kI)
-#undef CASE8K
-            default: break;
-        }
-        return fail(PSS_EUNSUPPORTED, "four-step: N=%lld too large", (long long)N);
     }
     // 2^14 .. 2^16: N1 = 16 columns, rows of N/16
     k.N1 = 16;
@@ -4035,7 +3750,6 @@ int64_t pss_workspace_bytes(int32_t nchan, int64_t nsamp) {
 int pss_run(const PssPipeline *p, void *stream) {
     int rc = validate(p);
     if (rc) return rc;
-    batches_setting();
     hipStream_t st = (hipStream_t)stream;
     KP k;
     memset(&k, 0, sizeof(k));
@@ -4064,7 +3778,6 @@ int pss_run(const PssPipeline *p, void *stream) {
             row = const_cast<float *>(p->inj_box);
         }
     }
-    if (p->htab) return run_fallback(k, st);        // baseband transfer function
     if (is_pow2(N) && N >= 64 && N <= 8192) return run_single(k, st);
     if (is_pow2(N) && N >= 16384 && N <= (1ll << 24)) return run_fourstep(k, st, row);
     if (smooth_split(N) && p->null_mode != PSS_NULL_DELAYED) return run_smooth(k, st);

@@ -51,10 +51,12 @@ def test_baseband_golden_exact(tag, hip_lib):
         ISM().disperse(sig, dm)
 
 
-@pytest.mark.parametrize("N", [4096, 51200, 1 << 16, 100002])
+@pytest.mark.parametrize("N", [4096, 51200, 1 << 16, 100002, 20480, 1 << 22])
 def test_filter_rows_vs_numpy(N, hip_lib):
-    """The transfer-function run (direct DFT for N <= 8192, Bluestein above,
-    powers of two included) against numpy irfft(rfft(x) H) in float64."""
+    """The transfer-function run against numpy irfft(rfft(x) H) in float64:
+    single pass (4096), the pair four-step with H in the row pass (2^16,
+    2^22; the mixed-radix 10 x 2048 split at 20480), Bluestein (51200,
+    100002)."""
     import torch
     from psrsigsim_amd import _engine
     rng = np.random.default_rng(N)

@@ -2,8 +2,11 @@
 """NumPy model of the device's chi2(1) draws (diagnostic / statistics study).
 
 Philox4x32-R (Salmon et al. 2011; the device's pss::philox, R = 7) with the
-pipeline's keying -- counter (n >> 2, tag 0, channel, call << 4 | purpose),
-key = seed -- and the Box-Muller chi2(1) of pss::chi2_1x4.  It reproduces
+pipeline's keying -- counter (block, tag 0, channel, call << 4 | purpose),
+key = seed; block n >> 2 holds samples 4 (n >> 2) .. + 3 (the noise and
+replacement draws; the search pulses' draws of an N-sample row, N % 4 == 0,
+take block n mod N/4, element n div N/4: pss::pulse_draw, `layout="quarter"`
+below) -- and the Box-Muller chi2(1) of pss::chi2_1x4.  It reproduces
 the device stream bit for bit (a GPU test's KS statistic on device draws
 equals the model's to all printed digits), so the quality of the generator
 can be studied on the CPU at sample sizes no GPU test would use:
@@ -35,9 +38,9 @@ def philox(c0, c1, c2, c3, k0, k1, rounds):
     return c0, c1, c2, c3
 
 
-def chi2_1(n, chan, seed, call, purpose, rounds=7, form="cos2"):
-    """Draws n = 0 .. n-1 of global channel `chan`.  form "cos2" (the device
-    default, PSS_BM_ONE_TRIG=1): h (1 +- cos 4 pi v), h = -ln u, with the
+def chi2_1(n, chan, seed, call, purpose, rounds=7, form="cos2", layout="consecutive"):
+    """Draws n = 0 .. n-1 of global channel `chan`.  form "cos2" (the device's
+    sampler): h (1 +- cos 4 pi v), h = -ln u, with the
     fp32 roundings of the device's last three operations (so the cancellation
     of the small member of a pair is modelled); "two-trig": the previous
     -2 ln u cos^2 / sin^2 form, float64."""
@@ -52,10 +55,18 @@ def chi2_1(n, chan, seed, call, purpose, rounds=7, form="cos2"):
         c0, c1 = f32(np.cos(2 * np.pi * fr(fr2(r[1])))), f32(np.cos(2 * np.pi * fr(fr2(r[3]))))
         t0, t1 = h0 * c0, h1 * c1
         out = np.stack([h0 + t0, h0 - t0, h1 + t1, h1 - t1], 1).astype(np.float64)
-        return out.ravel()[:n]
+        return _arrange(out, n, layout)
     l0, l1 = -2 * np.log(u01(r[0])), -2 * np.log(u01(r[2]))
     v0, v1 = 2 * np.pi * fr(r[1]), 2 * np.pi * fr(r[3])
     out = np.stack([l0 * np.cos(v0) ** 2, l0 * np.sin(v0) ** 2, l1 * np.cos(v1) ** 2, l1 * np.sin(v1) ** 2], 1)
+    return _arrange(out, n, layout)
+
+
+def _arrange(out, n, layout):
+    """Samples from the [block][4] draws: consecutive (sample 4 m + e) or
+    the search pulses' quarter layout (sample m + e n/4, n % 4 == 0)."""
+    if layout == "quarter" and n % 4 == 0:
+        return out[:n // 4].T.ravel()
     return out.ravel()[:n]
 
 
@@ -72,7 +83,7 @@ def study(out):
     sel = psr.Profiles.calc_profiles((np.arange(n) / spp) % 1)[0] > 0.5
     lines = []
     for R, form in ((7, "cos2"), (7, "two-trig"), (10, "two-trig")):
-        ps = np.array([stats.kstest(chi2_1(n, 0, s, 1, 1, R, form)[sel], stats.chi2(1).cdf).pvalue
+        ps = np.array([stats.kstest(chi2_1(n, 0, s, 1, 1, R, form, layout="quarter")[sel], stats.chi2(1).cdf).pvalue
                        for s in range(1, 401)])
         lag = {}
         m1 = m2 = 0.0
