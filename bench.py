@@ -166,6 +166,25 @@ def c2_step(pss, nchan_total, shard, nsamp_log2, plan_group=None):
     return sig
 
 
+def s5_step(pss, nchan_total, shard, plan_group=None):
+    """The 5-smooth length 3 125 000 = 2^3 5^8 (the sample count of the
+    reference's own simulate fixture, tests/test_simulate.py:47-56): 64
+    channels by default, GaussProfile P = 5 ms, disperse(DM=100) + Arecibo
+    noise, through the radix-5 four-step (1250 x 2500)."""
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+    from psrsigsim_amd.ism import ISM
+    from psrsigsim_amd.telescope import telescope as T
+    sig = FilterBankSignal(1400, 400, Nsubband=nchan_total, fold=False, shard=shard, plan_group=plan_group)
+    psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
+    psr.make_pulses(sig, tobs=S5_NSAMP * TOBS_PER_SAMPLE)
+    ISM().disperse(sig, 100)
+    T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True)
+    return sig
+
+
+S5_NSAMP = 3125000
+
 WORKLOADS = {
     "c2": "C2: NANOGrav L-band search mode 512 ch x 2^20 samp, J1713+0747 DataProfile (P=1/218.81 Hz), "
           "disperse(DM=15.917131) + GBT Lband_GUPPI radiometer noise",
@@ -176,6 +195,8 @@ WORKLOADS = {
           "DataProfile, disperse(DM=13.3) + Arecibo noise, RCCL gather of the folded filterbank to rank 0",
     "c5": "C5 per GPU: 1024 ch x 2^24 samp (8192 ch over 8 GPUs), GaussProfile P=5 ms, disperse(DM=500) + "
           "Arecibo noise",
+    "s5": "5-smooth length: 64 ch x 3 125 000 samp (= 2^3 5^8, the reference simulate fixture's sample count), "
+          "GaussProfile P=5 ms, disperse(DM=100) + Arecibo noise (radix-5 four-step 1250 x 2500)",
 }
 
 
@@ -189,7 +210,7 @@ def dry_step(pss, nchan_total, shard, nsamp_log2, plan_group=None):
     psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
     ism = ISM()
     ism.scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
-    psr.make_pulses(sig, tobs=(1 << nsamp_log2) * TOBS_PER_SAMPLE)
+    psr.make_pulses(sig, tobs=((1 << nsamp_log2) if nsamp_log2 else S5_NSAMP) * TOBS_PER_SAMPLE)
     ism.disperse(sig, 100)
     _engine.plan_pipeline(sig, sig._pending, shard[1] - shard[0], shard[0])
     return sig
@@ -407,6 +428,11 @@ def main():
     if args.workload == "c4":
         args.log2n = None
         args.no_cpu = True
+    if args.workload == "s5":
+        if args.nchan == NCHAN:
+            args.nchan = 64
+        args.log2n = None
+        args.no_cpu = True
     if args.scaling is None:
         args.scaling = "weak" if args.workload == "c5" else "strong"
 
@@ -457,7 +483,7 @@ def main():
             dist.barrier()
         sync()
 
-    nsamp = 30720 if args.workload == "c4" else (1 << args.log2n)
+    nsamp = 30720 if args.workload == "c4" else (S5_NSAMP if args.workload == "s5" else (1 << args.log2n))
 
     def step():
         # the API prints the reference's user warnings (e.g. C4's "sample
@@ -486,6 +512,8 @@ def main():
             return c5_step(pss, total, shard, args.log2n, plan_group=pg)
         if args.workload == "c2":
             return c2_step(pss, total, shard, args.log2n, plan_group=pg)
+        if args.workload == "s5":
+            return s5_step(pss, total, shard, plan_group=pg)
         return c3_step(pss, total, shard, args.log2n, plan_group=pg)
 
     for _ in range(args.warmup):

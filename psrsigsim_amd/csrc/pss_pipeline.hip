@@ -1335,7 +1335,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                     for (int q = 0; q < RFL; ++q) {
                         const int k2 = jj + q * LRL;
                         int bm, k2m;
-                        if (j == 0) { bm = b; k2m = (row == 0) ? ((N2 - k2) & (N2 - 1)) : (N2 - 1 - k2); }
+                        if (j == 0) { bm = b; k2m = (row == 0) ? (((N2 & (N2 - 1)) == 0) ? ((N2 - k2) & (N2 - 1)) : (k2 ? N2 - k2 : 0)) : (N2 - 1 - k2); }
                         else        { bm = 1 - b; k2m = N2 - 1 - k2; }
                         bin(q, lds[LD::at(bm, k2m)]);
                     }
@@ -1365,7 +1365,7 @@ struct PairRows<N2, T, RList<F...>, RList<I...>> {
                         Zm = lds_ld(mbase - 8u * (uint32_t)(q * LRL));
                     } else {
                         int bm, k2m;
-                        if (j == 0) { bm = b; k2m = (row == 0) ? ((N2 - k2) & (N2 - 1)) : (N2 - 1 - k2); }
+                        if (j == 0) { bm = b; k2m = (row == 0) ? (((N2 & (N2 - 1)) == 0) ? ((N2 - k2) & (N2 - 1)) : (k2 ? N2 - k2 : 0)) : (N2 - 1 - k2); }
                         else        { bm = 1 - b; k2m = N2 - 1 - k2; }
                         Zm = lds[LD::at(bm, k2m)];
                     }
@@ -1576,7 +1576,7 @@ struct PairRowsSeq<N2, T, RList<F...>, RList<I...>> {
 #pragma unroll
                     for (int q = 0; q < RFL; ++q) {
                         const int i = ib * RFL + q, k2 = jj + q * LRL;
-                        const int k2m = (row == 0) ? ((N2 - k2) & (N2 - 1)) : (N2 - 1 - k2);
+                        const int k2m = (row == 0) ? (((N2 & (N2 - 1)) == 0) ? ((N2 - k2) & (N2 - 1)) : (k2 ? N2 - k2 : 0)) : (N2 - 1 - k2);
                         const cf Z = v[i], Zm = lds[LD::at(0, k2m)];
                         const cf Sa = make_float2(Z.x + Zm.x, Z.y - Zm.y);
                         const cf Sb = make_float2(Z.y + Zm.y, Zm.x - Z.x);
@@ -1835,6 +1835,107 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
     // strides of 64 N2 samples.  Bitwise the values of passA<true>.
     // ------------------------------------------------------------------
     static constexpr bool kWaveA = kWaveCols && kMergeTw && kItemsExact && RF0 == 16 && (N1 % 64 == 0);
+    // The wave's column: profile x draws straight into the first stage's
+    // input registers (register ib R0 + q holds row lane + 64 ib + LR q,
+    // Fft::load's mapping; a Philox block covers rows r + e N1/4 = registers
+    // + 4 e, R0 = 16: N1/4 = 4 LR), phases by a walk in strides of LR rows.
+    template <bool SHARED>
+    __device__ static __forceinline__ void wave_column(const KP &k, cf (&v)[E], const float4 (*ptab)[kFastNint],
+                                                       int lane, uint32_t n2, uint32_t ca, float dna, float dnb) {
+        static_assert(RF0 == 16, "wave-local pass A: radix-16 first stage");
+        constexpr int LR = N1 / RF0;
+        const PssPipeline &p = k.p;
+        const uint32_t N2 = (uint32_t)k.N2, cb = ca + 1u;
+        const Rng g(p.seed, p.call_gen, P_PULSE);
+        uint32_t dlo;
+        uint64_t dhi;
+        phase_delta_n(p, (uint64_t)LR * (uint64_t)N2, dlo, dhi);
+        const uint32_t M = p.knot_m;
+#pragma unroll
+        for (int ib = 0; ib < E / RF0; ++ib) {
+            // profile values of the rows, in the register of their row
+            PhaseWalk w;
+            w.start(p, (uint32_t)(lane + 64 * ib) * N2 + n2);   // N <= 2^24
+#pragma unroll
+            for (int q = 0; q < RF0; ++q) {
+                uint32_t iv;
+                float u;
+                if (q) w.step(dlo, dhi, M);
+                w.get_full(iv, u);       // fast_source(): nint == knot_m
+                const float4 A = ptab[0][iv];
+                const float pa = fmaf(fmaf(fmaf(A.x, u, A.y), u, A.z), u, A.w);
+                float pb = pa;
+                if constexpr (!SHARED) {
+                    const float4 Bc = ptab[1][iv];
+                    pb = fmaf(fmaf(fmaf(Bc.x, u, Bc.y), u, Bc.z), u, Bc.w);
+                }
+                v[ib * RF0 + q] = make_float2(pa, pb);
+            }
+            // times the draws: block of row lane + 64 ib + LR q (q < 4)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t m = (uint32_t)(lane + 64 * ib + LR * q) * N2 + n2;
+                const float4 qa = chi2_1x4(g.bits(m, ca, 0u), dna);
+                const float4 qb = chi2_1x4(g.bits(m, cb, 0u), dnb);
+                const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    cf &x = v[ib * RF0 + q + 4 * e];
+                    x = make_float2(x.x * va[e], x.y * vb[e]);
+                }
+            }
+        }
+    }
+    // The column FFT's last stage (radix RFL at Ns = N1 / RFL) with the
+    // four-step twiddle W_N^{n2 k1} merged in (passA's merged stage): output
+    // m of butterfly jj is k1 = jj + Ns m; phases in exact 32-bit fixed point.
+    __device__ static __forceinline__ void last_stage_tw(const KP &k, cf (&v)[E], int lane, uint32_t n2) {
+        constexpr int NsL = N1 / RFL;
+        constexpr int LG1 = __builtin_ctz((unsigned)N1);
+        const int LGN = __builtin_ctzll((unsigned long long)k.N);        // N = 2^LGN here
+        const uint32_t A = n2 << (32 - LGN);                              // n2 / N (2^-32 rev)
+        cf U[RFL];
+#pragma unroll
+        for (int m = 1; m < RFL; ++m) U[m] = expi_rev(-fix32_to_rev(A * (uint32_t)(NsL * m)));
+#pragma unroll
+        for (int ib = 0; ib < E / RFL; ++ib) {
+            const uint32_t jj = (uint32_t)(lane + 64 * ib);              // < NsL
+            const uint32_t X0 = jj * A, S = jj << (32 - LG1);
+            cf *a = v + ib * RFL;
+#pragma unroll
+            for (int q = 0; q < RFL; ++q) a[q] = cmul(a[q], expi_rev(-fix32_to_rev(X0 + (uint32_t)q * S)));
+            dft<RFL, false>(a);
+#pragma unroll
+            for (int m = 1; m < RFL; ++m) a[m] = cmul(a[m], U[m]);
+        }
+    }
+    // Setup shared by the wave-local pass A kernels: block, pair, PCHIP rows
+    // of the pair staged in LDS (and tw16 filled); ends with the barrier.
+    template <bool SHARED>
+    __device__ static __forceinline__ void wave_setup(const KP &k, float4 (*ptab)[kFastNint], cf *tw16, int tid,
+                                                      int &pr, int64_t &n20, uint32_t &ca, float &dna, float &dnb) {
+        tw16_fill(tw16, tid, T);
+        int cbx;
+        xcd_block(cbx, pr);
+        const int ra = 2 * pr - k.poff, rb = ra + 1;
+        const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
+        n20 = (int64_t)cbx * B;
+        const PssPipeline &p = k.p;
+        ca = (uint32_t)(p.chan0 + ra);
+        const int pra = (p.prof_rows == 1) ? 0 : (int)ca - p.prof_row0;
+        const int prb = (p.prof_rows == 1) ? 0 : (int)ca + 1 - p.prof_row0;
+        const int nint = p.nint, last = p.prof_rows - 1;
+        const int rowa = min(max(pra, 0), last), rowb = min(max(prb, 0), last);
+        const float4 *prof = reinterpret_cast<const float4 *>(p.prof);
+        for (int i = tid; i < nint; i += T) {
+            ptab[0][i] = prof[(int64_t)rowa * nint + i];
+            if constexpr (!SHARED) ptab[1][i] = prof[(int64_t)rowb * nint + i];
+        }
+        // draw_norm, or 0 for a pair's missing channel (shard / band edges)
+        dna = hasa ? p.draw_norm : 0.f;
+        dnb = hasb ? p.draw_norm : 0.f;
+        __syncthreads();                // the tables (tw16 is first read in the FFT's second stage)
+    }
     template <bool SHARED>
     __device__ static void passA_wave(const KP &k) {
         static_assert(kWaveA, "wave-local pass A: one wave per column");
@@ -1842,102 +1943,143 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         __shared__ cf tw16[kTw16Size];
         __shared__ float4 ptab[SHARED ? 1 : 2][kFastNint];
         const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-        tw16_fill(tw16, tid, T);
-        int cbx, pr;
-        xcd_block(cbx, pr);
-        const int ra = 2 * pr - k.poff, rb = ra + 1;
-        const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
-        const int64_t n20 = (int64_t)cbx * B;
-        const int64_t N2 = k.N2;
-        const PssPipeline &p = k.p;
-        const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
-        const int pra = (p.prof_rows == 1) ? 0 : (int)ca - p.prof_row0, prb = (p.prof_rows == 1) ? 0 : (int)cb - p.prof_row0;
-        const Rng g(p.seed, p.call_gen, P_PULSE);
-        {
-            const int nint = p.nint, last = p.prof_rows - 1;
-            const int rowa = min(max(pra, 0), last), rowb = min(max(prb, 0), last);
-            const float4 *prof = reinterpret_cast<const float4 *>(p.prof);
-            for (int i = tid; i < nint; i += T) {
-                ptab[0][i] = prof[(int64_t)rowa * nint + i];
-                if constexpr (!SHARED) ptab[SHARED ? 0 : 1][i] = prof[(int64_t)rowb * nint + i];
-            }
-        }
-        __syncthreads();                // the tables (tw16 is first read in the FFT's second stage)
-        const float dna = hasa ? p.draw_norm : 0.f, dnb = hasb ? p.draw_norm : 0.f;
+        int pr;
+        int64_t n20;
+        uint32_t ca;
+        float dna, dnb;
+        wave_setup<SHARED>(k, ptab, tw16, tid, pr, n20, ca, dna, dnb);
         const uint32_t n2 = (uint32_t)(n20 + wv);
         cf v[E];
-        {
-            // register ib R0 + q holds row lane + 64 ib + LR q (the first
-            // stage's input mapping, Fft::load); a Philox block covers rows
-            // r + e N1/4 = registers + 4 e (R0 = 16: N1/4 = 4 LR)
-            static_assert(RF0 == 16, "wave-local pass A: radix-16 first stage");
-            constexpr int LR = N1 / RF0;
-            uint32_t dlo;
-            uint64_t dhi;
-            phase_delta_n(p, (uint64_t)LR * (uint64_t)N2, dlo, dhi);
-            const uint32_t M = p.knot_m;
-#pragma unroll
-            for (int ib = 0; ib < E / RF0; ++ib) {
-                // profile values of the rows, in the register of their row
-                PhaseWalk w;
-                w.start(p, (uint32_t)(lane + 64 * ib) * (uint32_t)N2 + n2);   // N <= 2^24
-#pragma unroll
-                for (int q = 0; q < RF0; ++q) {
-                    uint32_t iv;
-                    float u;
-                    if (q) w.step(dlo, dhi, M);
-                    w.get_full(iv, u);       // fast_source(): nint == knot_m
-                    const float4 A = ptab[0][iv];
-                    const float pa = fmaf(fmaf(fmaf(A.x, u, A.y), u, A.z), u, A.w);
-                    float pb = pa;
-                    if constexpr (!SHARED) {
-                        const float4 Bc = ptab[SHARED ? 0 : 1][iv];
-                        pb = fmaf(fmaf(fmaf(Bc.x, u, Bc.y), u, Bc.z), u, Bc.w);
-                    }
-                    v[ib * RF0 + q] = make_float2(pa, pb);
-                }
-                // times the draws: block of row lane + 64 ib + LR q (q < 4)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t m = (uint32_t)(lane + 64 * ib + LR * q) * (uint32_t)N2 + n2;
-                    const float4 qa = chi2_1x4(g.bits(m, ca, 0u), dna);
-                    const float4 qb = chi2_1x4(g.bits(m, cb, 0u), dnb);
-                    const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        cf &x = v[ib * RF0 + q + 4 * e];
-                        x = make_float2(x.x * va[e], x.y * vb[e]);
-                    }
-                }
-            }
-        }
+        wave_column<SHARED>(k, v, ptab, lane, n2, ca, dna, dnb);
         // column FFT (wave-local) with the four-step twiddle merged into the
         // last stage: as passA
         cf *wl = lds + wv * LdsC::RS;
         FW::template run_head_tw<false, 1, F...>(v, wl, lane, tw16);
-        {
-            constexpr int NsL = N1 / RFL;
-            constexpr int LG1 = __builtin_ctz((unsigned)N1);
-            const int LGN = __builtin_ctzll((unsigned long long)k.N);        // N = 2^LGN here
-            const uint32_t A = n2 << (32 - LGN);                              // n2 / N (2^-32 rev)
-            cf U[RFL];
-#pragma unroll
-            for (int m = 1; m < RFL; ++m) U[m] = expi_rev(-fix32_to_rev(A * (uint32_t)(NsL * m)));
-#pragma unroll
-            for (int ib = 0; ib < E / RFL; ++ib) {
-                const uint32_t jj = (uint32_t)(lane + 64 * ib);              // < NsL
-                const uint32_t X0 = jj * A, S = jj << (32 - LG1);
-                cf *a = v + ib * RFL;
-#pragma unroll
-                for (int q = 0; q < RFL; ++q) a[q] = cmul(a[q], expi_rev(-fix32_to_rev(X0 + (uint32_t)q * S)));
-                dft<RFL, false>(a);
-#pragma unroll
-                for (int m = 1; m < RFL; ++m) a[m] = cmul(a[m], U[m]);
-            }
-        }
+        last_stage_tw(k, v, lane, n2);
         FW::template store<RFL>(v, wl, lane);
         __syncthreads();
         spill_block(k, lds, tid, pr, n20);
+    }
+
+    // ------------------------------------------------------------------
+    // The same with HALF the LDS (C3's 1024 x 4096 split: 1024-point
+    // columns, radices 16 / 16 / 4, 8 columns): 47 KB per workgroup, three
+    // workgroups per CU -- 6 waves per SIMD instead of 4.
+    //   * the two in-column Stockham exchanges through a wave-private 4-KB
+    //     half, one register half per round (writer j's register q feeds
+    //     reader 16 (j & 3) + q after stage 1; reader 16 (q & 3) + (j & 15),
+    //     register 4 (q >> 2) + (j >> 4) after stage 2);
+    //   * the spill in two halves of 512 rows through [512][8] blocks whose
+    //     column pairs are swizzled by (row >> 2) & 3.
+    // Every layout here is conflict-free for its accesses; the values are
+    // passA_wave's bit for bit.
+    // ------------------------------------------------------------------
+    static constexpr bool kWaveHalf = kWaveA && N1 == 1024 && B == 8 && T == 512 && sizeof...(F) == 3 && RFL == 4;
+    __device__ static __forceinline__ int hblk(int r, int c) {
+        return r * 8 + 2 * ((c >> 1) ^ ((r >> 2) & 3)) + (c & 1);
+    }
+    template <bool SHARED>
+    __device__ static void passA_wave6(const KP &k) {
+        static_assert(kWaveHalf, "half-LDS wave pass A: the 1024 x 4096 split");
+        __shared__ __align__(128) cf X[512 * 8];
+        __shared__ cf tw16[kTw16Size];
+        __shared__ float4 ptab[SHARED ? 1 : 2][kFastNint];
+        const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+        int pr;
+        int64_t n20;
+        uint32_t ca;
+        float dna, dnb;
+        wave_setup<SHARED>(k, ptab, tw16, tid, pr, n20, ca, dna, dnb);
+        const uint32_t n2 = (uint32_t)(n20 + wv);
+        cf v[16];
+        wave_column<SHARED>(k, v, ptab, lane, n2, ca, dna, dnb);
+        const uint32_t wb = lds_byte(X) + 4096u * (uint32_t)wv;
+        const uint32_t ul = (uint32_t)lane;
+        // stage 1 (radix 16 over q, Ns = 1: no twiddles)
+        dft<16, false>(v);
+        {
+            // round rd moves registers 8 rd + qq of every lane; its readers
+            // are the lanes with (lane & 8) == 8 rd, each taking all 16 of its
+            // inputs.  Layout [qq][b = j & 3][j >> 2], inputs XORed by
+            // 4 (b >> 1) ^ qq.
+            const uint32_t b = ul & 3u;
+            const uint32_t W = wb + 128u * b + 8u * ((ul >> 2) ^ (4u * (b >> 1)));
+            const uint32_t rb = ul >> 4, qq = ul & 7u;
+            const uint32_t R = wb + 512u * qq + 128u * rb + 8u * ((4u * (rb >> 1)) ^ qq);
+            cf n[16];
+#pragma unroll
+            for (int rd = 0; rd < 2; ++rd) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) lds_st((W ^ (8u * (uint32_t)j)) + 512u * (uint32_t)j, v[8 * rd + j]);
+                stage_sync<true>();
+                if (((ul >> 3) & 1u) == (uint32_t)rd) {
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) n[q] = lds_ld(R ^ (8u * (uint32_t)q));
+                }
+                stage_sync<true>();
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = n[q];
+        }
+        // stage 2 (radix 16, Ns = 16: table twiddles W_256^{k q}, k = lane & 15)
+        {
+            const cf *t = tw16 + (lane & 15) * kTw16Pitch;
+#pragma unroll
+            for (int q = 1; q < 16; ++q) v[q] = cmul(v[q], t[q]);
+            dft<16, false>(v);
+        }
+        {
+            // round rd moves outputs q = 8 rd + qq: slot 4 (qq >> 2) + (j >> 4)
+            // of reader 16 (qq & 3) + (j & 15), at (P ^ 8 (qq & 3)) +
+            // 2048 (qq >> 2) + 128 (qq & 3); the reader's slot s (layout
+            // [8 slots][64 readers], low reader bits XORed by 4 (s & 3) +
+            // (reader >> 4)) is its register 8 rd + s
+            const uint32_t h4 = ul >> 4;
+            const uint32_t P = wb + 512u * h4 + ((8u * (ul & 15u)) ^ (32u * h4));
+            const uint32_t rbase = wb + 8u * (16u * h4 + ((ul & 15u) ^ h4));
+#pragma unroll
+            for (int rd = 0; rd < 2; ++rd) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t qj = (uint32_t)j;
+                    lds_st((P ^ (8u * (qj & 3u))) + 2048u * (qj >> 2) + 128u * (qj & 3u), v[8 * rd + j]);
+                }
+                stage_sync<true>();
+                cf m[8];
+#pragma unroll
+                for (int s = 0; s < 8; ++s) m[s] = lds_ld((rbase ^ (32u * (uint32_t)(s & 3))) + 512u * (uint32_t)s);
+                stage_sync<true>();
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[8 * rd + j] = m[j];
+            }
+        }
+        // stage 3 (radix 4, Ns = 256) with the four-step twiddle
+        last_stage_tw(k, v, lane, n2);
+        // spill: register 4 ib + m holds k1 = lane + 64 ib + 256 m; halves of 512 rows
+        cf *Y = k.Yd + (int64_t)pr * pstride(k);
+        const int64_t RP = rpitch(k);
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+            __syncthreads();            // (hf = 0: every wave's exchanges done; 1: half 0 stored)
+#pragma unroll
+            for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+                for (int mm = 0; mm < 2; ++mm) X[hblk(lane + 64 * ib + 256 * mm, wv)] = v[4 * ib + 2 * hf + mm];
+            __syncthreads();
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                // 32-lane groups: 32 consecutive rows of one 4-column group
+                const int it = tid + t * T, gq = it >> 5;
+                const int b4 = (gq & 1) * 4, r = (gq >> 1) * 32 + (it & 31);
+                const float4 lo = *reinterpret_cast<const float4 *>(X + hblk(r, b4));
+                const float4 hi = *reinterpret_cast<const float4 *>(X + hblk(r, b4 + 2));
+                const int64_t k1 = 512 * hf + r;
+                PSS_DASSERT(k1 * RP + n20 + b4 + 4 <= pstride(k));
+                float4 *dst = reinterpret_cast<float4 *>(Y + k1 * RP + n20 + b4);
+                dst[0] = lo;
+                dst[1] = hi;
+            }
+        }
     }
     // The spill of a column block from LDS (natural k1 per column row):
     // 16-B stores of 4 columns per row k1, 32 consecutive rows per 32-lane group.
@@ -2395,6 +2537,8 @@ template <typename C, int T, bool SHARED>
 __global__ __launch_bounds__(T) void k_pairA_fast(KP k) { C::template passA<true, SHARED>(k); }
 template <typename C, int T, bool SHARED>
 __global__ __launch_bounds__(T) void k_pairA_wave(KP k) { C::template passA_wave<SHARED>(k); }
+template <typename C, int T, bool SHARED>
+__global__ __launch_bounds__(T, 6) void k_pairA_wave6(KP k) { C::template passA_wave6<SHARED>(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairC(KP k) { C::passC(k); }
 template <typename C, int T>
@@ -3043,7 +3187,18 @@ static inline bool smooth_col(int64_t n1) {
         default: return false;
     }
 }
+// 5-smooth lengths with few factors of two take an LDS four-step with
+// radix-5 stages both ways: 3 125 000 = 2^3 5^8 (the sample count of the
+// reference's own simulate fixture, tests/test_simulate.py:47-56) as 1250
+// columns (2 x 5^4) x rows of 2500 (4 x 5^4).
+static inline bool smooth5_split(int64_t n, int64_t *N1 = nullptr, int64_t *N2 = nullptr) {
+    if (n != 3125000) return false;
+    if (N1) *N1 = 1250;
+    if (N2) *N2 = 2500;
+    return true;
+}
 static inline bool smooth_split(int64_t n, int64_t *N1 = nullptr, int64_t *N2 = nullptr) {
+    if (smooth5_split(n, N1, N2)) return true;
     if (n <= 0 || (n & 1) || is_pow2(n) || n > (1ll << 24)) return false;
     int v2 = __builtin_ctzll((unsigned long long)n);
     const int m = v2 - 1 < 13 ? v2 - 1 : 13;            // keep N1 even
@@ -3257,6 +3412,18 @@ constexpr int xrs_read(int B) { return B >= 32 ? 1 : 16; }
 // gain nothing from the swizzle and the XOR addressing costs VALU)
 constexpr int xrs_write(int B) { return -1; }
 
+// Pass A of the 1024 x 4096 split: the half-LDS 6-wave kernel (1, default)
+// or the 64-KB one (PSS_PASSA=4); a same-box A/B switch until one of them
+// is removed
+static bool wave6_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("PSS_PASSA");
+        v = (e && atoi(e) == 4) ? 0 : 1;
+    }
+    return v != 0;
+}
+
 struct SideStreams {
     hipStream_t s[2];
     hipEvent_t ev[40];
@@ -3356,9 +3523,17 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
         }
     }
     if (launched) {
-    } else if constexpr (PC::kItemsExact) {
+    } else if constexpr (PC::kItemsExact && N1 % 4 == 0) {
         if (fast_source(k.p)) {
-            if constexpr (PC::kWaveA) {
+            if constexpr (PC::kWaveHalf) {
+                if (wave6_enabled()) {
+                    if (k.p.prof_rows == 1) k_pairA_wave6<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
+                    else k_pairA_wave6<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
+                } else {
+                    if (k.p.prof_rows == 1) k_pairA_wave<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
+                    else k_pairA_wave<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
+                }
+            } else if constexpr (PC::kWaveA) {
                 if (k.p.prof_rows == 1) k_pairA_wave<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
                 else k_pairA_wave<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
             } else {
@@ -3501,6 +3676,12 @@ static int run_smooth(KP &k, hipStream_t st) {
     if (!smooth_split(k.N, &n1, &n2)) return fail(PSS_EUNSUPPORTED, "N=%lld", (long long)k.N);
     k.N1 = n1;
     k.N2 = n2;
+    if (n1 == 1250 && n2 == 2500) {
+        // 4-column blocks (2500 = 4 x 625) of 250 threads, 20 values each
+        using C1250 = RList<2, 5, 5, 5, 5>;
+        return launch_pair<1250, 4, 250, C1250, C1250, 2500, 250, RList<5, 5, 5, 5, 4>, RList<4, 5, 5, 5, 5>, 250, 4,
+                           250>(k, st, nullptr);
+    }
     switch (n1) {
         case 6:  return launch_smooth_n2<6, RList<2, 3>, RList<3, 2>, 256>(k, st);
         case 10: return launch_smooth_n2<10, RList<2, 5>, RList<5, 2>, 256>(k, st);

@@ -76,7 +76,10 @@ def test_shard_invariance_bitwise(log2n, hip_lib):
 @pytest.mark.parametrize("nchan,log2n,null,dm", [(3, 16, True, 100), (4, 17, True, 100), (5, 14, True, 100),
                                                 (2, 16, False, 100), (3, 22, True, 100),
                                                 # C5's per-GPU geometry: 2^24 (2048 x 8192 split), DM 500
-                                                (2, 24, True, 500)])
+                                                (2, 24, True, 500),
+                                                # 3 125 000 = 2^3 5^8 (radix-5 four-step 1250 x 2500; fast
+                                                # pass C, generic pass A; no delayed null off 2^m lengths)
+                                                (3, None, False, 100)])
 def test_fast_path_bitwise_equals_generic(nchan, log2n, null, dm, hip_lib):
     """The fast-path kernels (Philox df=1, no injection: the north-star
     configuration) against the generic kernels, bit for bit."""
@@ -91,7 +94,7 @@ def test_fast_path_bitwise_equals_generic(nchan, log2n, null, dm, hip_lib):
         pss.seed(11)
         sig = FilterBankSignal(1400, 400, Nsubband=nchan, fold=False)
         psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
-        psr.make_pulses(sig, tobs=(1 << log2n) * 20.48e-6)
+        psr.make_pulses(sig, tobs=(1 << log2n) * 20.48e-6 if log2n else 64.0)   # 64 s: 3 125 000 samples
         ISM().disperse(sig, dm)
         if null:
             psr.null(sig, 0.2)
@@ -100,7 +103,9 @@ def test_fast_path_bitwise_equals_generic(nchan, log2n, null, dm, hip_lib):
 
     L = _lib.lib()
     fast = run()
-    if log2n >= 22:
+    if log2n is None:
+        assert fast.shape[1] == 3125000
+    if (log2n or 22) >= 22:
         # run to run: a kernel reading LDS it did not write (stale from an
         # earlier workgroup) shows up here even when both paths share it
         np.testing.assert_array_equal(run(), fast)

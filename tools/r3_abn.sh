@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box comparison of several builds on the C3 bench line (round-robin,
 # 2 rounds), after the GPU parity tests of the product library.
-# usage: tools/r3_abn.sh TAG "name=lib name=lib ..." [skip-tests]   (lib "-" = product)
+# usage: tools/r3_abn.sh TAG "name=lib[@VAR=val] ..." [skip-tests]   (lib "-" = product)
 set -o pipefail
 TAG=${1:-abn}
 LIBS=$2
@@ -16,7 +16,9 @@ fi
 for i in 1 2; do
   for nl in $LIBS; do
     t=${nl%%=*}; lib=${nl#*=}
+    envs=""; case "$lib" in *@*) envs=${lib#*@}; lib=${lib%%@*} ;; esac   # name=lib@VAR=val[,VAR2=val]
     if [ "$lib" = - ]; then unset PSS_LIB_PATH; else export PSS_LIB_PATH=$lib; fi
+    unset PSS_PASSA; for e in ${envs//,/ }; do export "$e"; done
     timeout -k 10 300 python bench.py --no-cpu --steps 20 > $OUT/ab_${TAG}_${t}_$i.json 2> $OUT/ab_${TAG}_${t}_$i.err \
       || { echo "$t $i failed"; tail -3 $OUT/ab_${TAG}_${t}_$i.err; exit 1; }
     python -c "import json; d=json.load(open('$OUT/ab_${TAG}_${t}_$i.json')); p=d['gpu_power'] or {}; print('$t', $i, d['ms_per_step'], d['step_ms_steady'], round(d['gpu_kernel_ms_per_step'],2), {k: v['avg_ms'] for k, v in d['kernels'].items()}, p.get('sclk_mhz_median'), p.get('socket_w_median'))"
