@@ -22,7 +22,13 @@ OUT_DEBUG = os.path.join(HERE, "libpss_hip_debug.so")
 ARCH = os.environ.get("PSS_OFFLOAD_ARCH", "gfx950")
 # -fno-slp-vectorize: packed f32 (v_pk_*) issues at half rate on gfx950 and
 # costs register-pair moves; scalar f32 is cheaper here.
-FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-slp-vectorize"]
+# -ffp-contract=on: a multiply-add fuses only within one source expression,
+# never across statements, so a value's rounding does not depend on the code
+# around it (HIP's default fuses e.g. the wave pass A's profile x draw
+# product into the first butterfly, which the LDS-staged kernels cannot: the
+# fast and generic kernels would differ by an ulp; ~1 % of pass A's VALU).
+FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-slp-vectorize",
+         "-ffp-contract=on"]
 
 
 def source_hash(extra=()):

@@ -175,8 +175,10 @@ __device__ __forceinline__ float4 chi2_1x4(uint4 r, float scale = 1.0f) {
     const float h1 = kl * __builtin_amdgcn_logf(u01(r.z));
     const float c0 = __builtin_amdgcn_cosf(frac23(r.y << 1));                 // cos(2 pi (2v mod 1))
     const float c1 = __builtin_amdgcn_cosf(frac23(r.w << 1));
-    const float t0 = h0 * c0, t1 = h1 * c1;
-    return make_float4(h0 + t0, h0 - t0, h1 + t1, h1 - t1);
+    // explicit fused forms: left to the compiler, h + h c contracts or not
+    // depending on the surrounding code, and the fast and generic kernels
+    // would draw values an ulp apart
+    return make_float4(fmaf(h0, c0, h0), fmaf(-h0, c0, h0), fmaf(h1, c1, h1), fmaf(-h1, c1, h1));
 }
 
 // Four N(0, 1) draws from one Philox block (Box-Muller pairs

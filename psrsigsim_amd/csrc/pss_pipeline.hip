@@ -3412,16 +3412,16 @@ constexpr int xrs_read(int B) { return B >= 32 ? 1 : 16; }
 // gain nothing from the swizzle and the XOR addressing costs VALU)
 constexpr int xrs_write(int B) { return -1; }
 
-// Pass A of the 1024 x 4096 split: the half-LDS 6-wave kernel (1, default)
-// or the 64-KB one (PSS_PASSA=4); a same-box A/B switch until one of them
-// is removed
-static bool wave6_enabled() {
+// Pass A of the wave-column splits: the half-LDS 6-wave kernel (6, default
+// at C3), the 64-KB wave kernel (4) or the LDS-staged passA<true> (0); a
+// same-box A/B switch (PSS_PASSA) until the slower ones are removed
+static int passa_variant() {
     static int v = -1;
     if (v < 0) {
         const char *e = getenv("PSS_PASSA");
-        v = (e && atoi(e) == 4) ? 0 : 1;
+        v = e ? atoi(e) : 6;
     }
-    return v != 0;
+    return v;
 }
 
 struct SideStreams {
@@ -3525,8 +3525,11 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     if (launched) {
     } else if constexpr (PC::kItemsExact && N1 % 4 == 0) {
         if (fast_source(k.p)) {
-            if constexpr (PC::kWaveHalf) {
-                if (wave6_enabled()) {
+            if (passa_variant() == 0) {
+                if (k.p.prof_rows == 1) k_pairA_fast<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
+                else k_pairA_fast<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
+            } else if constexpr (PC::kWaveHalf) {
+                if (passa_variant() == 6) {
                     if (k.p.prof_rows == 1) k_pairA_wave6<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
                     else k_pairA_wave6<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
                 } else {

@@ -53,8 +53,9 @@ def chi2_1(n, chan, seed, call, purpose, rounds=7, form="cos2", layout="consecut
         fr2 = lambda x: ((x << np.uint64(1)) & MASK).astype(np.uint64)
         h0, h1 = f32(-np.log(u01(r[0]))), f32(-np.log(u01(r[2])))
         c0, c1 = f32(np.cos(2 * np.pi * fr(fr2(r[1])))), f32(np.cos(2 * np.pi * fr(fr2(r[3]))))
-        t0, t1 = h0 * c0, h1 * c1
-        out = np.stack([h0 + t0, h0 - t0, h1 + t1, h1 - t1], 1).astype(np.float64)
+        # fused h (1 +- c): the product exact in float64, one fp32 rounding
+        d0, d1 = h0.astype(np.float64) * c0, h1.astype(np.float64) * c1
+        out = np.stack([f32(h0 + d0), f32(h0 - d0), f32(h1 + d1), f32(h1 - d1)], 1).astype(np.float64)
         return _arrange(out, n, layout)
     l0, l1 = -2 * np.log(u01(r[0])), -2 * np.log(u01(r[2]))
     v0, v1 = 2 * np.pi * fr(r[1]), 2 * np.pi * fr(r[3])
