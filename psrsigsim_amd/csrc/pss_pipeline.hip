@@ -496,16 +496,19 @@ __device__ __forceinline__ void draw4(const Rng &g, int64_t n0, uint32_t c, floa
 }
 
 // Search-mode chi2(1) pulse draw of sample n in a row of N samples (P_PULSE,
-// df = 1; `scale` = draw_norm folded into the sampler).  Keying: for N % 4
-// == 0 the Philox block m < N/4 holds samples m + e N/4 (e < 4, its four draws
-// in order) -- the rows n1, n1 + N1/4, n1 + N1/2, n1 + 3 N1/4 of one four-step
-// column, so a column's values are drawn where the column is transformed
-// (passA_wave: no cross-wave transpose of the generated samples); otherwise
-// block n >> 2 holds samples 4 (n >> 2) .. + 3.  Every path draws through this
-// rule (or the same blocks), so results do not depend on the path.
+// df = 1; `scale` = draw_norm folded into the sampler).  Keying: Philox block
+// n >> 2 holds samples 4 (n >> 2) .. + 3 (the LDS-staged fast pass A draws a
+// block per 4 consecutive samples of a row), except for rows of N >= 2^24,
+// N % 4 == 0 (C5's 2048 x 8192 split): there block m < N/4 holds samples
+// m + e N/4 (e < 4, its four draws in order) -- the rows n1, n1 + N1/4,
+// n1 + N1/2, n1 + 3 N1/4 of one four-step column, so a column's values are
+// drawn where the column is transformed (passA_wave: no cross-wave
+// transpose of the generated samples).  Every path draws through this rule
+// (or the same blocks), so results do not depend on the path.
+__host__ __device__ constexpr bool pulse_quarter(int64_t N) { return (N & 3) == 0 && N >= (int64_t(1) << 24); }
 __device__ __forceinline__ void pulse_block(int64_t n, int64_t N, uint32_t &m, uint32_t &tag, uint32_t &e) {
     uint64_t mm;
-    if ((N & 3) == 0) {
+    if (pulse_quarter(N)) {
         const uint64_t Q = (uint64_t)N >> 2;
         e = (uint32_t)((uint64_t)n / Q);
         mm = (uint64_t)n - (uint64_t)e * Q;
@@ -668,7 +671,7 @@ __device__ __forceinline__ void source4(const KP &k, int r, int64_t n0, int cnt,
                 // chi2(1) draws with draw_norm folded into the sampler (as the
                 // fast pass A draws them: bitwise the same values)
                 Rng g(p.seed, p.call_gen, P_PULSE);
-                if ((k.N & 3) == 0) {
+                if (pulse_quarter(k.N)) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) x[i] = (i < cnt) ? pulse_draw(g, n0 + i, k.N, c, p.draw_norm) : 0.f;
                 } else {
@@ -1696,34 +1699,39 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             // draw_norm, or 0 for a pair's missing channel (shard / band
             // edges): the multiply the sample needs anyway zeroes it, no select
             const float dna = hasa ? p.draw_norm : 0.f, dnb = hasb ? p.draw_norm : 0.f;
-            // item = Philox block m = n1 N2 + n20 + b (n1 < N1/4): the samples
-            // m + e N/4 = rows n1 + e N1/4 of column b (pulse_draw's keying),
-            // their phases by a walk in strides of N/4
-            static_assert(N1 % 4 == 0, "fast pass A: quarter-row items");
-            constexpr int NQ = N1 / 4;
+            // item = 4 consecutive samples n .. n + 3 of row n1 (Philox block
+            // n >> 2: pulse_draw's keying below 2^24), phases by a unit walk
             uint32_t dlo;
             uint64_t dhi;
-            phase_delta_n(p, (uint64_t)NQ * (uint64_t)N2, dlo, dhi);
+            phase_delta(p, dlo, dhi);
             const uint32_t M = p.knot_m;
 #pragma unroll
             for (int t = 0; t < ITEMS; ++t) {
-                // lanes = consecutive rows n1 of one column: the LDS writes
-                // below are conflict-free (this loop touches no global
-                // memory, so its item order is free)
+                // lanes = consecutive rows n1 (of one 4-column group where
+                // N1 % 64 == 0): the transposed LDS writes below are
+                // conflict-free (this loop touches no global memory, so its
+                // item order is free)
                 const int it = tid + t * T;
-                const int n1 = it % NQ, b = it / NQ;
-                const uint32_t m = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b;   // N <= 2^24
+                int n1, b4;
+                if constexpr (N1 % 64 == 0) {
+                    n1 = it % N1;
+                    b4 = (it / N1) * 4;
+                } else {
+                    n1 = it / (B / 4);
+                    b4 = (it - n1 * (B / 4)) * 4;
+                }
+                const uint32_t n = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4;   // N < 2^24
                 // draws scaled by draw_norm (0 for a pair's missing channel) in the sampler
-                const float4 qa = chi2_1x4(g.bits(m, ca, 0u), dna);
-                const float4 qb = chi2_1x4(g.bits(m, cb, 0u), dnb);
+                const float4 qa = chi2_1x4(g.bits(n >> 2, ca, 0u), dna);
+                const float4 qb = chi2_1x4(g.bits(n >> 2, cb, 0u), dnb);
                 const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
                 PhaseWalk w;
-                w.start(p, m);
+                w.start(p, n);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
+                for (int i = 0; i < 4; ++i) {
                     uint32_t iv;
                     float u;
-                    if (e) w.step(dlo, dhi, M);
+                    if (i) w.step(dlo, dhi, M);
                     w.get_full(iv, u);       // fast_source(): nint == knot_m
                     const float4 A = ptab[0][iv];
                     const float pa = fmaf(fmaf(fmaf(A.x, u, A.y), u, A.z), u, A.w);
@@ -1732,7 +1740,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                         const float4 Bc = ptab[1][iv];
                         pb = fmaf(fmaf(fmaf(Bc.x, u, Bc.y), u, Bc.z), u, Bc.w);
                     }
-                    lds[LdsC::at(b, n1 + e * NQ)] = make_float2(pa * va[e], pb * vb[e]);
+                    lds[LdsC::at(b4 + i, n1)] = make_float2(pa * va[i], pb * vb[i]);
                 }
             }
         } else
@@ -1961,126 +1969,6 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         spill_block(k, lds, tid, pr, n20);
     }
 
-    // ------------------------------------------------------------------
-    // The same with HALF the LDS (C3's 1024 x 4096 split: 1024-point
-    // columns, radices 16 / 16 / 4, 8 columns): 47 KB per workgroup, three
-    // workgroups per CU -- 6 waves per SIMD instead of 4.
-    //   * the two in-column Stockham exchanges through a wave-private 4-KB
-    //     half, one register half per round (writer j's register q feeds
-    //     reader 16 (j & 3) + q after stage 1; reader 16 (q & 3) + (j & 15),
-    //     register 4 (q >> 2) + (j >> 4) after stage 2);
-    //   * the spill in two halves of 512 rows through [512][8] blocks whose
-    //     column pairs are swizzled by (row >> 2) & 3.
-    // Every layout here is conflict-free for its accesses; the values are
-    // passA_wave's bit for bit.
-    // ------------------------------------------------------------------
-    static constexpr bool kWaveHalf = kWaveA && N1 == 1024 && B == 8 && T == 512 && sizeof...(F) == 3 && RFL == 4;
-    __device__ static __forceinline__ int hblk(int r, int c) {
-        return r * 8 + 2 * ((c >> 1) ^ ((r >> 2) & 3)) + (c & 1);
-    }
-    template <bool SHARED>
-    __device__ static void passA_wave6(const KP &k) {
-        static_assert(kWaveHalf, "half-LDS wave pass A: the 1024 x 4096 split");
-        __shared__ __align__(128) cf X[512 * 8];
-        __shared__ cf tw16[kTw16Size];
-        __shared__ float4 ptab[SHARED ? 1 : 2][kFastNint];
-        const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-        int pr;
-        int64_t n20;
-        uint32_t ca;
-        float dna, dnb;
-        wave_setup<SHARED>(k, ptab, tw16, tid, pr, n20, ca, dna, dnb);
-        const uint32_t n2 = (uint32_t)(n20 + wv);
-        cf v[16];
-        wave_column<SHARED>(k, v, ptab, lane, n2, ca, dna, dnb);
-        const uint32_t wb = lds_byte(X) + 4096u * (uint32_t)wv;
-        const uint32_t ul = (uint32_t)lane;
-        // stage 1 (radix 16 over q, Ns = 1: no twiddles)
-        dft<16, false>(v);
-        {
-            // round rd moves registers 8 rd + qq of every lane; its readers
-            // are the lanes with (lane & 8) == 8 rd, each taking all 16 of its
-            // inputs.  Layout [qq][b = j & 3][j >> 2], inputs XORed by
-            // 4 (b >> 1) ^ qq.
-            const uint32_t b = ul & 3u;
-            const uint32_t W = wb + 128u * b + 8u * ((ul >> 2) ^ (4u * (b >> 1)));
-            const uint32_t rb = ul >> 4, qq = ul & 7u;
-            const uint32_t R = wb + 512u * qq + 128u * rb + 8u * ((4u * (rb >> 1)) ^ qq);
-            cf n[16];
-#pragma unroll
-            for (int rd = 0; rd < 2; ++rd) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) lds_st((W ^ (8u * (uint32_t)j)) + 512u * (uint32_t)j, v[8 * rd + j]);
-                stage_sync<true>();
-                if (((ul >> 3) & 1u) == (uint32_t)rd) {
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) n[q] = lds_ld(R ^ (8u * (uint32_t)q));
-                }
-                stage_sync<true>();
-            }
-#pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = n[q];
-        }
-        // stage 2 (radix 16, Ns = 16: table twiddles W_256^{k q}, k = lane & 15)
-        {
-            const cf *t = tw16 + (lane & 15) * kTw16Pitch;
-#pragma unroll
-            for (int q = 1; q < 16; ++q) v[q] = cmul(v[q], t[q]);
-            dft<16, false>(v);
-        }
-        {
-            // round rd moves outputs q = 8 rd + qq: slot 4 (qq >> 2) + (j >> 4)
-            // of reader 16 (qq & 3) + (j & 15), at (P ^ 8 (qq & 3)) +
-            // 2048 (qq >> 2) + 128 (qq & 3); the reader's slot s (layout
-            // [8 slots][64 readers], low reader bits XORed by 4 (s & 3) +
-            // (reader >> 4)) is its register 8 rd + s
-            const uint32_t h4 = ul >> 4;
-            const uint32_t P = wb + 512u * h4 + ((8u * (ul & 15u)) ^ (32u * h4));
-            const uint32_t rbase = wb + 8u * (16u * h4 + ((ul & 15u) ^ h4));
-#pragma unroll
-            for (int rd = 0; rd < 2; ++rd) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const uint32_t qj = (uint32_t)j;
-                    lds_st((P ^ (8u * (qj & 3u))) + 2048u * (qj >> 2) + 128u * (qj & 3u), v[8 * rd + j]);
-                }
-                stage_sync<true>();
-                cf m[8];
-#pragma unroll
-                for (int s = 0; s < 8; ++s) m[s] = lds_ld((rbase ^ (32u * (uint32_t)(s & 3))) + 512u * (uint32_t)s);
-                stage_sync<true>();
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[8 * rd + j] = m[j];
-            }
-        }
-        // stage 3 (radix 4, Ns = 256) with the four-step twiddle
-        last_stage_tw(k, v, lane, n2);
-        // spill: register 4 ib + m holds k1 = lane + 64 ib + 256 m; halves of 512 rows
-        cf *Y = k.Yd + (int64_t)pr * pstride(k);
-        const int64_t RP = rpitch(k);
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-            __syncthreads();            // (hf = 0: every wave's exchanges done; 1: half 0 stored)
-#pragma unroll
-            for (int ib = 0; ib < 4; ++ib)
-#pragma unroll
-                for (int mm = 0; mm < 2; ++mm) X[hblk(lane + 64 * ib + 256 * mm, wv)] = v[4 * ib + 2 * hf + mm];
-            __syncthreads();
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                // 32-lane groups: 32 consecutive rows of one 4-column group
-                const int it = tid + t * T, gq = it >> 5;
-                const int b4 = (gq & 1) * 4, r = (gq >> 1) * 32 + (it & 31);
-                const float4 lo = *reinterpret_cast<const float4 *>(X + hblk(r, b4));
-                const float4 hi = *reinterpret_cast<const float4 *>(X + hblk(r, b4 + 2));
-                const int64_t k1 = 512 * hf + r;
-                PSS_DASSERT(k1 * RP + n20 + b4 + 4 <= pstride(k));
-                float4 *dst = reinterpret_cast<float4 *>(Y + k1 * RP + n20 + b4);
-                dst[0] = lo;
-                dst[1] = hi;
-            }
-        }
-    }
     // The spill of a column block from LDS (natural k1 per column row):
     // 16-B stores of 4 columns per row k1, 32 consecutive rows per 32-lane group.
     __device__ static __forceinline__ void spill_block(const KP &k, const cf *lds, int tid, int pr, int64_t n20) {
@@ -2537,8 +2425,6 @@ template <typename C, int T, bool SHARED>
 __global__ __launch_bounds__(T) void k_pairA_fast(KP k) { C::template passA<true, SHARED>(k); }
 template <typename C, int T, bool SHARED>
 __global__ __launch_bounds__(T) void k_pairA_wave(KP k) { C::template passA_wave<SHARED>(k); }
-template <typename C, int T, bool SHARED>
-__global__ __launch_bounds__(T, 6) void k_pairA_wave6(KP k) { C::template passA_wave6<SHARED>(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairC(KP k) { C::passC(k); }
 template <typename C, int T>
@@ -3412,18 +3298,6 @@ constexpr int xrs_read(int B) { return B >= 32 ? 1 : 16; }
 // gain nothing from the swizzle and the XOR addressing costs VALU)
 constexpr int xrs_write(int B) { return -1; }
 
-// Pass A of the wave-column splits: the half-LDS 6-wave kernel (6, default
-// at C3), the 64-KB wave kernel (4) or the LDS-staged passA<true> (0); a
-// same-box A/B switch (PSS_PASSA) until the slower ones are removed
-static int passa_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("PSS_PASSA");
-        v = e ? atoi(e) : 6;
-    }
-    return v;
-}
-
 struct SideStreams {
     hipStream_t s[2];
     hipEvent_t ev[40];
@@ -3525,23 +3399,20 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     if (launched) {
     } else if constexpr (PC::kItemsExact && N1 % 4 == 0) {
         if (fast_source(k.p)) {
-            if (passa_variant() == 0) {
-                if (k.p.prof_rows == 1) k_pairA_fast<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
-                else k_pairA_fast<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
-            } else if constexpr (PC::kWaveHalf) {
-                if (passa_variant() == 6) {
-                    if (k.p.prof_rows == 1) k_pairA_wave6<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
-                    else k_pairA_wave6<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
-                } else {
+            // C5's split (quarter-keyed pulses, N >= 2^24): the wave-local
+            // kernel; otherwise the LDS-staged passA<true>
+            bool wave = false;
+            if constexpr (PC::kWaveA) wave = pulse_quarter(k.N);
+            if (wave) {
+                if constexpr (PC::kWaveA) {
                     if (k.p.prof_rows == 1) k_pairA_wave<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
                     else k_pairA_wave<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
                 }
-            } else if constexpr (PC::kWaveA) {
-                if (k.p.prof_rows == 1) k_pairA_wave<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
-                else k_pairA_wave<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
-            } else {
+            } else if (!pulse_quarter(k.N)) {
                 if (k.p.prof_rows == 1) k_pairA_fast<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
                 else k_pairA_fast<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
+            } else {
+                k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
             }
         } else {
             k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);

@@ -5,7 +5,7 @@ Philox4x32-R (Salmon et al. 2011; the device's pss::philox, R = 7) with the
 pipeline's keying -- counter (block, tag 0, channel, call << 4 | purpose),
 key = seed; block n >> 2 holds samples 4 (n >> 2) .. + 3 (the noise and
 replacement draws; the search pulses' draws of an N-sample row, N % 4 == 0,
-take block n mod N/4, element n div N/4: pss::pulse_draw, `layout="quarter"`
+take block n mod N/4, element n div N/4 for N >= 2^24: pss::pulse_draw, `layout="quarter"`
 below) -- and the Box-Muller chi2(1) of pss::chi2_1x4.  It reproduces
 the device stream bit for bit (a GPU test's KS statistic on device draws
 equals the model's to all printed digits), so the quality of the generator
@@ -65,8 +65,8 @@ def chi2_1(n, chan, seed, call, purpose, rounds=7, form="cos2", layout="consecut
 
 def _arrange(out, n, layout):
     """Samples from the [block][4] draws: consecutive (sample 4 m + e) or
-    the search pulses' quarter layout (sample m + e n/4, n % 4 == 0)."""
-    if layout == "quarter" and n % 4 == 0:
+    the search pulses' quarter layout (sample m + e n/4, n % 4 == 0, n >= 2^24)."""
+    if layout == "quarter" and n % 4 == 0 and n >= (1 << 24):
         return out[:n // 4].T.ravel()
     return out.ravel()[:n]
 

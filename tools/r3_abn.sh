@@ -19,7 +19,7 @@ for i in 1 2; do
     envs=""; case "$lib" in *@*) envs=${lib#*@}; lib=${lib%%@*} ;; esac   # name=lib@VAR=val[,VAR2=val]
     if [ "$lib" = - ]; then unset PSS_LIB_PATH; else export PSS_LIB_PATH=$lib; fi
     unset PSS_PASSA; for e in ${envs//,/ }; do export "$e"; done
-    timeout -k 10 300 python bench.py --no-cpu --steps 20 > $OUT/ab_${TAG}_${t}_$i.json 2> $OUT/ab_${TAG}_${t}_$i.err \
+    timeout -k 10 300 python bench.py --no-cpu --steps ${AB_STEPS:-20} ${AB_ARGS:-} > $OUT/ab_${TAG}_${t}_$i.json 2> $OUT/ab_${TAG}_${t}_$i.err \
       || { echo "$t $i failed"; tail -3 $OUT/ab_${TAG}_${t}_$i.err; exit 1; }
     python -c "import json; d=json.load(open('$OUT/ab_${TAG}_${t}_$i.json')); p=d['gpu_power'] or {}; print('$t', $i, d['ms_per_step'], d['step_ms_steady'], round(d['gpu_kernel_ms_per_step'],2), {k: v['avg_ms'] for k, v in d['kernels'].items()}, p.get('sclk_mhz_median'), p.get('socket_w_median'))"
   done

@@ -14,4 +14,4 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
     "${KARG[@]}" > $OUT/gpu_tests_$TAG.log 2>&1
 rc=$?; echo "tests rc=$rc"; grep -E "^FAILED|passed|failed|Error" $OUT/gpu_tests_$TAG.log | tail -8
 [ $rc -ne 0 ] && exit $rc
-[ -n "$LIBS" ] && bash tools/r3_abn.sh $TAG "$LIBS" skip-tests
+if [ -n "$LIBS" ]; then bash tools/r3_abn.sh $TAG "$LIBS" skip-tests; fi
