@@ -3397,7 +3397,7 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
         }
     }
     if (launched) {
-    } else if constexpr (PC::kItemsExact && N1 % 4 == 0) {
+    } else if constexpr (PC::kItemsExact) {
         if (fast_source(k.p)) {
             // C5's split (quarter-keyed pulses, N >= 2^24): the wave-local
             // kernel; otherwise the LDS-staged passA<true>

@@ -78,7 +78,7 @@ def test_shard_invariance_bitwise(log2n, hip_lib):
                                                 # C5's per-GPU geometry: 2^24 (2048 x 8192 split), DM 500
                                                 (2, 24, True, 500),
                                                 # 3 125 000 = 2^3 5^8 (radix-5 four-step 1250 x 2500; fast
-                                                # pass C, generic pass A; no delayed null off 2^m lengths)
+                                                # passes A and C; no delayed null off 2^m lengths)
                                                 (3, None, False, 100)])
 def test_fast_path_bitwise_equals_generic(nchan, log2n, null, dm, hip_lib):
     """The fast-path kernels (Philox df=1, no injection: the north-star

@@ -1,5 +1,6 @@
 """Host work of one C3 step issued on an idle GPU (the first timed step's
-critical path): wall time and cProfile of the API calls.  GPU box only."""
+critical path): wall time and cProfile of the API calls.  GPU box only.
+usage: tools/host_first.py [nchan]"""
 import cProfile
 import os
 import pstats
@@ -10,20 +11,21 @@ import torch
 import psrsigsim_amd as pss
 import bench
 
+NCH = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
 for _ in range(2):
-    s = bench.c3_step(pss, 2048, None, 22)
+    s = bench.c3_step(pss, NCH, None, 22)
     s.data
     del s
 torch.cuda.synchronize()
 for _ in range(2):
     t = time.perf_counter()
-    s = bench.c3_step(pss, 2048, None, 22)
+    s = bench.c3_step(pss, NCH, None, 22)
     print("host %.2f ms" % ((time.perf_counter() - t) * 1e3))
     torch.cuda.synchronize()
     del s
 pr = cProfile.Profile()
 pr.enable()
-s = bench.c3_step(pss, 2048, None, 22)
+s = bench.c3_step(pss, NCH, None, 22)
 pr.disable()
 torch.cuda.synchronize()
 pstats.Stats(pr).sort_stats("cumtime").print_stats(30)
