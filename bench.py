@@ -168,9 +168,11 @@ def c2_step(pss, nchan_total, shard, nsamp_log2, plan_group=None):
 
 def s5_step(pss, nchan_total, shard, plan_group=None):
     """The 5-smooth length 3 125 000 = 2^3 5^8 (the sample count of the
-    reference's own simulate fixture, tests/test_simulate.py:47-56): 64
-    channels by default, GaussProfile P = 5 ms, disperse(DM=100) + Arecibo
-    noise, through the radix-5 four-step (1250 x 2500)."""
+    reference's own simulate fixture, tests/test_simulate.py:47-56): 256
+    channels by default (one rank's share of the C3 band at 8 GPUs; 64
+    channels leave ~7 % of the step to per-step host work), GaussProfile
+    P = 5 ms, disperse(DM=100) + Arecibo noise, through the radix-5
+    four-step (1250 x 2500)."""
     from psrsigsim_amd.signal import FilterBankSignal
     from psrsigsim_amd.pulsar import Pulsar, GaussProfile
     from psrsigsim_amd.ism import ISM
@@ -195,7 +197,7 @@ WORKLOADS = {
           "DataProfile, disperse(DM=13.3) + Arecibo noise, RCCL gather of the folded filterbank to rank 0",
     "c5": "C5 per GPU: 1024 ch x 2^24 samp (8192 ch over 8 GPUs), GaussProfile P=5 ms, disperse(DM=500) + "
           "Arecibo noise",
-    "s5": "5-smooth length: 64 ch x 3 125 000 samp (= 2^3 5^8, the reference simulate fixture's sample count), "
+    "s5": "5-smooth length: 256 ch x 3 125 000 samp (= 2^3 5^8, the reference simulate fixture's sample count), "
           "GaussProfile P=5 ms, disperse(DM=100) + Arecibo noise (radix-5 four-step 1250 x 2500)",
 }
 
@@ -430,7 +432,7 @@ def main():
         args.no_cpu = True
     if args.workload == "s5":
         if args.nchan == NCHAN:
-            args.nchan = 64
+            args.nchan = 256
         args.log2n = None
         args.no_cpu = True
     if args.scaling is None:
@@ -606,7 +608,7 @@ def main():
                                        "/ ms_per_step / (8 TB/s x n_gpus)"}
         # measured HBM bytes per launch of this kernel (rocprofv3 PMC passes,
         # tools/pmc_round.sh + tools/pmc_traffic.py; C3 size only)
-        for rnd in ("r03", "r02"):
+        for rnd in ("r04", "r03", "r02"):
             tj = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
             if args.workload == "c3" and C == NCHAN and nsamp == (1 << LOG2N) and os.path.exists(tj):
                 t = json.load(open(tj)).get(dom)
