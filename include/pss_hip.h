@@ -189,6 +189,9 @@ const char *pss_build_hash(void);
 /* PSS_FLAG_DIRECT_DFT sends the fallback lengths N > 8192 through the O(N^2)
  * direct DFT instead of the Bluestein (chirp-z) path (test hook). */
 #define PSS_FLAG_DIRECT_DFT 2
+/* PSS_FLAG_NULL_F32 keeps the packed (direct / Bluestein) paths' delayed-null
+   decisions in fp32 (no float64 re-evaluation near the threshold).          */
+#define PSS_FLAG_NULL_F32 4
 int pss_set_flags(int flags);
 int pss_last_error(char *buf, size_t n);
 

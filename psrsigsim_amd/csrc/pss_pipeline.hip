@@ -2640,6 +2640,117 @@ __global__ __launch_bounds__(256) void k_fb_epilogue(KP k) {
 }
 
 // ---------------------------------------------------------------------------
+// Delayed null on the packed (direct / Bluestein) paths, decided in float64.
+// These paths carry the box row through the channel's complex transform as
+// its imaginary part, so the fp32 mask shares the error of the data (fold-mode
+// rows peak at ~1e4; the boxes are chi2(Nfold) values of that size themselves)
+// and a few percent of the samples sit within that error of the threshold 1.
+// For those samples (|mask - 1| < max(1e-3, 3e-5 x the row's largest |value|),
+// a generous multiple of the transform's measured ~2e-6 relative error) the
+// mask is re-evaluated in float64 from the box row's spectrum B(k) (once per
+// run, channel independent):
+//   m(n) = ( B_0 + 2 sum_{0<k<N/2} Re(B_k e^{2 pi i k (n/N - s)}) + B_{N/2} nyq (-1)^n ) / N,
+// s = the channel's ramp (frac(delay/N)), nyq its mask Nyquist factor -- the
+// reference's shift_t of the box row by the total delay (pulsar.py:306-330,
+// utils.py:17-59) -- and its decision m > 1 replaces the fp32 one (encoded as
+// mask 2 / 0 for the epilogue).  One wave per candidate sample, the bins split
+// over the lanes (phasor recurrences from one sincospi per lane), a wave sum.
+// Even N <= kRefineMaxN (the O(N x nnz) box spectrum), no scattering tail
+// (an extension whose packed path also filters the mask).
+// ---------------------------------------------------------------------------
+static constexpr int64_t kRefineMaxN = 1 << 17;
+
+__global__ __launch_bounds__(256) void k_tw64(int64_t N, double2 *tw) {
+    for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; n < N; n += (int64_t)gridDim.x * 256) {
+        double sn, cs;
+        sincospi(2.0 * (double)n / (double)N, &sn, &cs);
+        tw[n] = make_double2(cs, sn);                    // e^{+2 pi i n / N}
+    }
+}
+
+// B_k = sum_n box[n] e^{-2 pi i k n / N}, k <= N/2 (float64; the tile loop is
+// uniform over the workgroup, so skipping zero box samples does not diverge)
+__global__ __launch_bounds__(256) void k_null_bspec(const float *box, int64_t N, const double2 *tw, double2 *B) {
+    __shared__ float tile[1024];
+    const int64_t K = N / 2 + 1;
+    const int64_t kb = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t kk = kb < K ? kb : 0;
+    double re = 0.0, im = 0.0;
+    for (int64_t base = 0; base < N; base += 1024) {
+        const int cnt = (int)min((int64_t)1024, N - base);
+        __syncthreads();
+        for (int i = threadIdx.x; i < cnt; i += 256) tile[i] = box[base + i];
+        __syncthreads();
+        int64_t m = (kk * base) % N;
+        for (int i = 0; i < cnt; ++i) {
+            const float b = tile[i];
+            if (b != 0.0f) {
+                const double2 w = tw[m];
+                re += (double)b * w.x;
+                im -= (double)b * w.y;
+            }
+            m += kk;
+            if (m >= N) m -= N;
+        }
+    }
+    if (kb < K) B[kb] = make_double2(re, im);
+}
+
+// per row: the largest |value| of the packed inverse (data and mask parts),
+// the scale of its fp32 error (mx zeroed by the host; positive floats order
+// as their bit patterns)
+__global__ __launch_bounds__(256) void k_row_absmax(const cf *W1, int64_t N, unsigned int *mx) {
+    const int r = blockIdx.y;
+    float v = 0.0f;
+    for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; n < N; n += (int64_t)gridDim.x * 256) {
+        const cf z = W1[(int64_t)r * N + n];
+        v = fmaxf(v, fmaxf(fabsf(z.x), fabsf(z.y)));
+    }
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(mx + r, __float_as_uint(v));
+}
+
+__global__ __launch_bounds__(256) void k_null_refine(KP k, cf *W1, const double2 *B, const unsigned int *mx) {
+    const int r = blockIdx.y, lane = threadIdx.x & 63;
+    const int64_t N = k.N, H = N / 2;
+    const float band = fmaxf(1e-3f, 3e-5f * __uint_as_float(mx[r]));
+    const double ramp = (double)k.p.ramp[r] * 5.421010862427522e-20;     // 2^-64
+    const double nyq = (double)k.p.nyq_im[r];
+    const int64_t nw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);       // this wave's 64 samples
+    const int64_t n = nw * 64 + lane;
+    cf *z = W1 + (int64_t)r * N;
+    const bool cand = n < N && fabsf(z[n < N ? n : 0].y - 1.0f) < band;
+    uint64_t todo = __ballot(cand);
+    while (todo) {
+        const int src = __ffsll((long long)todo) - 1;
+        todo &= todo - 1;
+        const int64_t ns = nw * 64 + src;
+        // per-bin phase step (revolutions): n/N - s
+        double phi = (double)ns / (double)N - ramp;
+        phi -= floor(phi);
+        // lane's bins k = 1 + lane + 64 j, phasor e^{2 pi i k phi} by recurrence
+        double sn, cs, s64, c64;
+        sincospi(2.0 * phi * (double)(1 + lane), &sn, &cs);
+        sincospi(2.0 * phi * 64.0, &s64, &c64);
+        double acc = 0.0;
+        for (int64_t kb = 1 + lane; kb < H; kb += 64) {
+            const double2 b = B[kb];
+            acc = fma(b.x, cs, fma(-b.y, sn, acc));
+            const double t = cs * c64 - sn * s64;
+            sn = cs * s64 + sn * c64;
+            cs = t;
+        }
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if (lane == src) {
+            double m = B[0].x + 2.0 * acc;
+            if (2 * H == N) m += B[H].x * nyq * ((ns & 1) ? -1.0 : 1.0);
+            m /= (double)N;
+            z[ns].y = m > 1.0 ? 2.0f : 0.0f;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // odd N (utils.shift_t only): the reference's irfft without n= returns
 // L = N - 1 samples -- the inverse of length L of the N-point spectrum's bins
 // 0..M (M = (N - 1)/2), bin M taken as L's Nyquist bin (real part only):
@@ -3119,6 +3230,7 @@ struct WsLayout {
     int64_t yd, mspec, ynode, nodes, bits, base, coef, misc, mbits, rtab, wlist, row, total;
     int64_t bs_chirp, bs_bhat, bs_z;   // Bluestein: w [N] | Bhat [M] | Z [nb][M] (cf)
     int64_t odd_tw;                    // odd N: exp(+2 pi i j / (N - 1)), j < N - 1 (cf)
+    int64_t rf_tw, rf_B, rf_mx;        // float64 null decisions: e^{2 pi i n/N} [N], B [N/2+1] (double2), row max [nchan]
 };
 
 static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
@@ -3156,6 +3268,11 @@ static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
             w.bs_chirp = o; o += al256(N * 8);
             w.bs_bhat = o;  o += al256(g.M * 8);
             w.bs_z = o;     o += al256(g.nb * g.M * 8);
+        }
+        if (!odd && N <= kRefineMaxN) {
+            w.rf_tw = o; o += al256(N * 16);
+            w.rf_B = o;  o += al256((N / 2 + 1) * 16);
+            w.rf_mx = o; o += al256((int64_t)nchan * 4);
         }
         if (smooth_split(N)) {
             // mixed-radix four-step (inside the same bytes: the direct path
@@ -3645,6 +3762,40 @@ static int bs_filter(const KP &k, BsArgs a, int64_t nb, hipStream_t st) {
     return PSS_OK;
 }
 
+// The float64 null decisions of the packed paths (k_null_refine), between
+// the inverse transform (W1 = data + i mask per row) and the epilogue.
+static bool refine_null(const KP &k) {
+    return k.p.null_mode == PSS_NULL_DELAYED && (k.N & 1) == 0 && k.N <= kRefineMaxN && !k.p.tail_a &&
+           !k.p.htab && !(g_flags & PSS_FLAG_NULL_F32);
+}
+
+static int launch_null_refine(KP &k, hipStream_t st) {
+    const WsLayout w = ws_layout(k.p.nchan, k.N, k.p.htab != nullptr);
+    char *base = reinterpret_cast<char *>(k.p.work);
+    cf *W1 = reinterpret_cast<cf *>(base);
+    double2 *tw = reinterpret_cast<double2 *>(base + w.rf_tw);
+    double2 *B = reinterpret_cast<double2 *>(base + w.rf_B);
+    unsigned int *mx = reinterpret_cast<unsigned int *>(base + w.rf_mx);
+    const float *box = k.p.inj_box;
+    if (!box) {
+        float *row = reinterpret_cast<float *>(base + w.row);
+        k_box_row<<<stream_grid(k.N, 1), dim3(256), 0, st>>>(k, row);
+        LAUNCHCHK();
+        box = row;
+    }
+    k_tw64<<<stream_grid(k.N, 1), dim3(256), 0, st>>>(k.N, tw);
+    LAUNCHCHK();
+    k_null_bspec<<<dim3((unsigned)((k.N / 2 + 1 + 255) / 256)), dim3(256), 0, st>>>(box, k.N, tw, B);
+    LAUNCHCHK();
+    HIPCHK(hipMemsetAsync(mx, 0, (size_t)k.p.nchan * 4, st));
+    k_row_absmax<<<dim3((unsigned)std::min<int64_t>(64, (k.N + 255) / 256), (unsigned)k.p.nchan), dim3(256), 0, st>>>(
+        W1, k.N, mx);
+    LAUNCHCHK();
+    k_null_refine<<<dim3((unsigned)((k.N + 255) / 256), (unsigned)k.p.nchan), dim3(256), 0, st>>>(k, W1, B, mx);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
 static int run_bluestein(KP &k, hipStream_t st) {
     const WsLayout w = ws_layout(k.p.nchan, k.N, k.p.htab != nullptr);
     const BsGeom g = bs_geom(k.p.nchan, k.N);
@@ -3675,6 +3826,7 @@ static int run_bluestein(KP &k, hipStream_t st) {
     a.dst = W1;
     a.mode = 0;
     if ((rc = bs_filter(k, a, g.nb, st))) return rc;
+    if (refine_null(k) && (rc = launch_null_refine(k, st))) return rc;
     k_fb_epilogue<<<ge, dim3(256), 0, st>>>(k);
     tk_end(st);
     LAUNCHCHK();
@@ -3694,6 +3846,10 @@ static int run_fallback(KP &k, hipStream_t st) {
     LAUNCHCHK();
     k_fb_dft<true><<<gd, dim3(256), 0, st>>>(k);
     LAUNCHCHK();
+    if (refine_null(k)) {
+        const int rc = launch_null_refine(k, st);
+        if (rc) return rc;
+    }
     k_fb_epilogue<<<g, dim3(256), 0, st>>>(k);
     tk_end(st);
     LAUNCHCHK();

@@ -42,11 +42,33 @@ AMBIG_REL_TABLE = 2e-6
 # 1.1e-4 -> 1.6e-5 (B1855 template): the ambiguity is the fp32 transform's
 # ~2e-6 relative error on a row of ~1e4 values thresholded at 1, not the
 # packing -- kept packed.)
-AMBIG_MAX_FRAC = {"table": 2e-3, "packed": 3e-2}
+# Packed lengths whose decisions the device re-evaluates in float64
+# (`k_null_refine`: even N <= 2^17 on the direct / Bluestein paths, no
+# scattering tail; not the single-workgroup 2^m <= 8192 kernel): what is left
+# is the rounding of the fp32 box values the device starts from, <= 6e-8 x
+# sum_j |box_j K(n - j)| (K the shift's interpolation kernel, L1 norm ~5 at
+# these N): band 5e-7 x the mask scale (+ AMBIG absolute).
+AMBIG_REL_P64 = 5e-7
+REFINE_MAX_N = 1 << 17
+REFINED = True      # False while the device runs with PSS_FLAG_NULL_F32 (tools)
+
+
+def packed64(n, case):
+    pow2 = n & (n - 1) == 0
+    return (REFINED and n % 2 == 0 and n <= REFINE_MAX_N and not (pow2 and n <= 8192)
+            and not any(op[0] == "scatter_tail" for op in case["ops"]))
+
+
+# "packed": the float64-decided packed lengths (C4's fold-mode geometry with a
+# delayed null: band 9.3e-4, no flips, against 1.9 % and up to 1.1e-4 flipped
+# with the fp32 decisions, tools/null_band_r4.py, profiles/r04/null_band.txt);
+# "packed_f32": the packed lengths the device still decides in fp32 (the
+# single-workgroup 2^m <= 8192 kernel, N > 2^17, the scattering tail)
+AMBIG_MAX_FRAC = {"table": 2e-3, "packed": 2e-3, "packed_f32": 3e-2}
 # fold mode (C4) boxes are chi2(Nfold ~ 1e4) values thresholded at 1: the
 # fp32 transform's ~2e-6 relative error (Bluestein) is ~0.02 absolute there,
 # so a few samples per 1e4 sit on the other side of the threshold
-FLIP_MAX_FRAC = {"table": 1e-5, "packed": 3e-4}
+FLIP_MAX_FRAC = {"table": 1e-5, "packed": 1e-5, "packed_f32": 3e-4}
 
 
 def _prof():
@@ -192,8 +214,11 @@ def oracle_exec(case, d):
                 if n >= (1 << 14) and n & (n - 1) == 0:
                     inj["ambig_path"] = "table"
                     band = AMBIG_REL_TABLE * np.max(np.abs(ms), axis=1)[:, None]
-                else:
+                elif packed64(n, case):
                     inj["ambig_path"] = "packed"
+                    band = AMBIG_REL_P64 * np.max(np.abs(ms), axis=1)[:, None]
+                else:
+                    inj["ambig_path"] = "packed_f32"
                     band = AMBIG_REL * np.maximum(pre_max, np.max(np.abs(ms), axis=1))[:, None]
                 inj["ambiguous"] = np.abs(ms - 1.0) < np.maximum(AMBIG, band)
         elif k == "observe":
@@ -360,7 +385,7 @@ def run_case(name, fused=True, case=None, seed=None):
         errs[last[-1][-1]] = _err(sig.data.cpu().numpy(), A["data_" + last[-1][-1]], amb["mask"])
     if _AMB["total"]:
         band = _AMB["band"] / _AMB["total"]
-        path = inj.get("ambig_path", "packed")
+        path = inj.get("ambig_path", "packed_f32")
         flipped = _AMB["flipped"] / _AMB["total"]
         STATS["null_flipped_frac"] = flipped
         STATS["ambiguous_band_frac"] = band

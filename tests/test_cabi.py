@@ -55,14 +55,17 @@ def test_workspace_sizes():
     wl = (n // 32) * 4
     assert L.pss_workspace_bytes(4, n) == 3 * n * 8 + table + 4 * n // 8 + 3 * 1024 + wl + n * 4
     assert L.pss_workspace_bytes(3, n) == 2 * n * 8 + table + 3 * n // 8 + 2 * 1024 + wl + n * 4
+    a = lambda b: ((b + 255) // 256) * 256
+    # even N <= 2^17 on the fallback paths: + the float64 null decisions'
+    # e^{2 pi i n/N} [N] and box spectrum [N/2 + 1] (double2), row maxima [nchan]
+    f64 = lambda n, nc: a(n * 16) + a((n // 2 + 1) * 16) + a(nc * 4)
     sp = 2 * 2 * 244 * 8 + 244 * 8                                   # fallback W1, W2, twiddles
-    assert L.pss_workspace_bytes(2, 244) == ((sp + 255) // 256) * 256 + 1024   # row: 976 B, aligned
+    assert L.pss_workspace_bytes(2, 244) == a(sp) + f64(244, 2) + 1024   # row: 976 B, aligned
     # Bluestein fallback (N > 8192, 2 x 5003): W1 only (forward and inverse
     # DFT fused through Z) | chirp [N] | Bhat [M = 32768] | one batch row [M]
     # (nb = max(1, nchan N / M)) | mask row
-    a = lambda b: ((b + 255) // 256) * 256
     n = 10006
-    assert L.pss_workspace_bytes(2, n) == a(2 * n * 8) + a(n * 8) + 2 * a(32768 * 8) + a(n * 4)
+    assert L.pss_workspace_bytes(2, n) == a(2 * n * 8) + f64(n, 2) + a(n * 8) + 2 * a(32768 * 8) + a(n * 4)
     # 8 x (2^20 - 2): M = 2^22, nb = 8 (2^20 - 2) // 2^21 = 3
     n = (1 << 20) - 2
     M = 1 << 21
@@ -71,7 +74,7 @@ def test_workspace_sizes():
     old = L.pss_set_flags(_lib.FLAG_DIRECT_DFT)
     try:
         n = 10006
-        assert L.pss_workspace_bytes(2, n) == a(5 * n * 8) + a(n * 8) + 2 * a(32768 * 8) + a(n * 4)
+        assert L.pss_workspace_bytes(2, n) == a(5 * n * 8) + f64(n, 2) + a(n * 8) + 2 * a(32768 * 8) + a(n * 4)
     finally:
         L.pss_set_flags(old)
 
