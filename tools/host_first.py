@@ -29,3 +29,4 @@ s = bench.c3_step(pss, NCH, None, 22)
 pr.disable()
 torch.cuda.synchronize()
 pstats.Stats(pr).sort_stats("cumtime").print_stats(30)
+pstats.Stats(pr).sort_stats("tottime").print_stats(40)
