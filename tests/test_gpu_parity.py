@@ -26,8 +26,8 @@ SIZES = [64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536, 1 << 17
          # mixed-radix four-step: N1 x N2 = 6 x 2048, 10 x 4096, 30 x 2048, 30 x 4096, 24 x 8192
          12288, 40960, 61440, 122880, 196608,
          # Bluestein (chirp-z) fallback: M1 x M2 = 8 x 4096 (2 x 5003), 64 x 4096,
-         # 1024 x 4096 (2^20 - 2), 2048 x 4096 (the reference simulate fixture's
-         # 3 125 000 = 2^3 5^8), 4096 x 8192 (2^24 - 2)
+         # 1024 x 4096 (2^20 - 2), 4096 x 8192 (2^24 - 2); and the reference
+         # simulate fixture's 3 125 000 = 2^3 5^8 (radix-5 four-step 1250 x 2500)
          10006, 100002, (1 << 20) - 2, 3125000, (1 << 24) - 2]
 
 

@@ -104,7 +104,8 @@ def test_simulate_equals_manual_calls(rate, hip_lib):
     """simulate() = the reference's call sequence (simulate.py:292-326) made
     by hand with the same seed: bitwise (one fused run either way).  The
     reference fixture's 1.5625 MHz gives 3 125 000 = 2^3 5^8 samples per
-    channel (Bluestein path); the 2048-bin variant is a power of two."""
+    channel (radix-5 four-step 1250 x 2500); the 2048-bin variant is a power
+    of two."""
     import psrsigsim_amd as pss
     from psrsigsim_amd.signal import FilterBankSignal
     from psrsigsim_amd.pulsar import Pulsar, GaussPortrait
