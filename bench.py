@@ -625,11 +625,12 @@ def main():
         if args.cpu_workers > 0:
             va, dta = cpu_baseline_allcore(args.cpu_workers, 2, args.log2n)
             cpu_all = {"value": round(va, 1), "unit": "channel-samples/s", "cores": args.cpu_workers,
-                       "kind": "port",
+                       "cpu_count": os.cpu_count(), "kind": "port",
                        "sample": "%d concurrent single-threaded processes x 2 ch x 2^%d samp of the same C3 "
                                  "pipeline (oracle/pss_cpu.py), slowest worker %.1f s" % (args.cpu_workers,
                                                                                          args.log2n, dta)}
-        cpu = {"value": round(v, 1), "unit": "channel-samples/s", "cores": 1, "kind": "port",
+        cpu = {"value": round(v, 1), "unit": "channel-samples/s", "cores": 1, "cpu_count": os.cpu_count(),
+               "kind": "port",
                "sample": "%d ch x 2^%d samp of the same C3 pipeline, oracle/pss_cpu.py (float64 NumPy, "
                          "reference call structure; like the reference it also builds observe's pre-noise "
                          "out copy, ~2%% of its time, which the GPU run elides when ret_resampsig=False), "

@@ -174,7 +174,23 @@ typedef struct PssPipeline {
                                interior knot, in the cell coordinate u) followed
                                by [nint] split points (u >= split: right cubic;
                                2 = no knot in the cell); knot_m = nint cells */
-    int32_t reserved1;
+    /* observe()'s RESAMPLED pre-noise copy, produced by the run itself
+       (telescope.py:108-125 down_sample / rebin, then :140-145 clip and cast):
+       out_len > 0 makes `out` [nchan][out_len] of kind out_kind, bin i = the
+       mean of the pre-noise samples [lo_i, hi_i), clipped from above at `clip`.
+       Every epilogue adds its samples' values into out_acc (float64 window
+       sums, zeroed by pss_run), a final small kernel divides, clips and casts:
+       no full-resolution copy, no separate resampling pass.                 */
+    int32_t out_len;        /* 0: `out` is the full [nchan][nsamp] copy         */
+    const int64_t *out_lo;  /* [out_len] window starts (utils.py:77-89's ceil
+                               edges), or NULL: uniform windows of out_step
+                               samples, lo_i = i * out_step (down_sample,
+                               utils.py:62-68)                                 */
+    const int64_t *out_hi;  /* [out_len] window ends (exclusive), or NULL       */
+    double out_step;        /* nominal window width: the bin of sample n is
+                               floor(n / out_step) or the one before it; an
+                               integer >= 1 when out_lo is NULL               */
+    double *out_acc;        /* [nchan][out_len] float64 scratch                 */
 } PssPipeline;
 
 /* Library / device info. */

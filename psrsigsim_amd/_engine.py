@@ -320,6 +320,14 @@ def build_pipeline(sig, pend, rows, chan0, data, out=None, ws_role="main"):
         p.out_kind = out["kind"]
         p.out = ptr(out["tensor"])
         p.clip = out["clip"]
+        win = out.get("windows")
+        if win is not None:
+            # observe()'s resampled copy, produced by the run (PssPipeline.out_len)
+            p.out_len = int(win["len"])
+            p.out_lo = ptr(win["lo"])
+            p.out_hi = ptr(win["hi"])
+            p.out_step = float(win["step"])
+            p.out_acc = ptr(win["acc"])
     return p, keep
 
 

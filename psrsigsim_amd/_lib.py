@@ -44,7 +44,8 @@ class PssPipeline(ctypes.Structure):
         ("inj_gen", c_vp), ("inj_box", c_vp), ("inj_rep", c_vp), ("inj_noise", c_vp),
         ("mask_ramp", c_vp),
         ("gen_amp", c_i32), ("prof_row0", c_i32), ("htab", c_vp), ("null_shift_dev", c_vp),
-        ("tail_a", c_vp), ("prof_split", c_i32), ("reserved1", c_i32),
+        ("tail_a", c_vp), ("prof_split", c_i32), ("out_len", c_i32), ("out_lo", c_vp), ("out_hi", c_vp),
+        ("out_step", ctypes.c_double), ("out_acc", c_vp),
     ]
 
 

@@ -727,6 +727,119 @@ __device__ __forceinline__ void source4(const KP &k, int r, int64_t n0, int cnt,
     }
 }
 
+// observe()'s resampled pre-noise copy (PssPipeline.out_len > 0): the
+// samples n0 .. n0 + cnt - 1 of row r added into the float64 sums of the
+// windows [lo_j, hi_j) that hold them (down_sample, utils.py:62-68: lo_j =
+// j f; rebin, utils.py:71-91: lo_j = ceil(j step), hi_j = ceil(j step + step)
+// clipped to N, so neighbouring windows may share a sample).  The edges are
+// recomputed from step with the host's float64 operations (out_lo / out_hi
+// serve the finalize kernel's counts); a window holding n is floor(n / step)
+// or the one before.  A lane's samples form a head piece (its first window)
+// and a tail piece (its last; pieces in between go straight to their
+// atomics); the head joins the previous lane's tail when they are the same
+// window, and the tails are summed over each run of lanes with the same
+// window -- a segmented reduction by doubling that only extends a sum over
+// lanes it has covered without a gap, and stops once no run is still
+// growing -- so one no-return float64 atomic leaves the wave per window
+// piece.  (Within-wave sums in fp32: at most 256 samples, summed as a tree.)
+// Waves whose lanes hold different rows (the single-workgroup kernel's row
+// batches) skip the cross-lane step.  k_out_finalize divides, clips and casts
+// (telescope.py:140-145).  All active lanes of a wave call it together (the
+// epilogues' item loops are wave-uniform up to their tails; inactive lanes
+// are masked out through the ballot).
+__device__ __forceinline__ void out_windows(const PssPipeline &p, int r, uint32_t N, uint32_t n0, int cnt,
+                                            const float (&v)[4]) {
+    const int lane = (int)__lane_id();
+    const uint64_t act = __ballot(1);
+    const uint32_t L = (uint32_t)p.out_len;
+    const bool uniform = p.out_lo == nullptr;
+    const double step = p.out_step;
+    const uint32_t f = (uint32_t)step;
+    double *acc = p.out_acc + (int64_t)r * L;
+    const uint32_t last = n0 + (uint32_t)cnt - 1u;
+    int64_t ja, jb;
+    if (uniform) {
+        ja = n0 / f;
+        jb = last / f;
+    } else {
+        const double inv = 1.0 / step;      // (wave-uniform: hoisted by the compiler)
+        ja = (int64_t)floor((double)n0 * inv) - 2;
+        jb = (int64_t)floor((double)last * inv) + 1;
+    }
+    ja = ja < 0 ? 0 : ja;
+    jb = jb > (int64_t)L - 1 ? (int64_t)L - 1 : jb;
+    uint32_t jH = 0xffffffffu, jT = 0xffffffffu;      // head / tail window, ~0: none
+    float sH = 0.f, sT = 0.f;
+    for (int64_t jj = ja; jj <= jb; ++jj) {
+        const uint32_t j = (uint32_t)jj;
+        uint32_t lo, hi;
+        if (uniform) {
+            lo = j * f;
+            hi = lo + f;
+        } else {
+            // two statements: the sum is not contracted into an fma
+            const double lb = (double)j * step;
+            const double rb = lb + step;
+            lo = (uint32_t)ceil(lb);
+            hi = (uint32_t)ceil(rb);
+            hi = hi > N ? N : hi;
+        }
+        float s = 0.f;
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t n = n0 + (uint32_t)i;
+            if (i < cnt && n >= lo && n < hi) {
+                s += v[i];
+                any = true;
+            }
+        }
+        if (!any) continue;
+        if (jT == 0xffffffffu) {
+            jH = jT = j;
+            sT = s;
+        } else {
+            if (jH == jT) sH = sT;                            // the first window becomes the head
+            else unsafeAtomicAdd(acc + jT, (double)sT);        // a window in the middle of the lane
+            jT = j;
+            sT = s;
+        }
+    }
+    const bool has_head = jT != 0xffffffffu && jH != jT;
+    const int r0 = __builtin_amdgcn_readfirstlane(r);
+    if (__ballot(r != r0) != 0ull) {
+        // lanes of several rows: no cross-lane merge
+        if (has_head) unsafeAtomicAdd(acc + jH, (double)sH);
+        if (jT != 0xffffffffu) unsafeAtomicAdd(acc + jT, (double)sT);
+        return;
+    }
+    // the head joins the previous lane's tail (the same window)
+    const uint32_t nxt_h = (uint32_t)__shfl_down((int)(has_head ? jH : 0xffffffffu), 1);
+    const float nxt_s = __shfl_down(sH, 1);
+    const uint32_t prv_t = (uint32_t)__shfl_up((int)jT, 1);
+    const bool nxt_ok = lane < 63 && ((act >> (lane + 1)) & 1ull);
+    const bool prv_ok = lane > 0 && ((act >> (lane - 1)) & 1ull);
+    if (jT != 0xffffffffu && nxt_ok && nxt_h == jT) sT += nxt_s;
+    if (has_head && !(prv_ok && prv_t == jH)) unsafeAtomicAdd(acc + jH, (double)sH);
+    // segmented sum of the tails over runs of lanes with one window
+    const uint32_t key = jT != 0xffffffffu ? jT : 0x80000000u + (uint32_t)lane;   // no tail: a key of its own
+    float sum = sT;
+    int len = 1;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t ok_ = (uint32_t)__shfl_down((int)key, d);
+        const bool grow = len == d && lane + d < 64 && ((act >> (lane + d)) & 1ull) && ok_ == key;
+        if (__ballot(grow) == 0ull) break;
+        const float os = __shfl_down(sum, d);
+        const int ol = __shfl_down(len, d);
+        if (grow) {
+            sum += os;
+            len += ol;
+        }
+    }
+    if (jT != 0xffffffffu && !(prv_ok && prv_t == key)) unsafeAtomicAdd(acc + jT, (double)sum);
+}
+
 // Epilogue for 4 consecutive samples: delayed-null replacement where the
 // shifted mask exceeds 1, the observe() pre-noise copy, radiometer noise, store.
 // `pre` holds the data value (FFT output already scaled by 1/N, or the source).
@@ -758,7 +871,9 @@ __device__ __forceinline__ void epilogue4(const KP &k, int r, int64_t n0, int cn
                 if (i < cnt && mask[i] > 1.0f) pre[i] = x[i];
         }
     }
-    if (p.out_kind == PSS_OUT_F32) {
+    if (p.out_kind != PSS_OUT_NONE && p.out_len > 0) {
+        out_windows(p, r, (uint32_t)k.N, (uint32_t)n0, cnt, pre);
+    } else if (p.out_kind == PSS_OUT_F32) {
         float *o = (float *)p.out + (int64_t)r * k.N;
 #pragma unroll
         for (int i = 0; i < 4; ++i) if (i < cnt) o[n0 + i] = (pre[i] > p.clip) ? p.clip : pre[i];
@@ -3018,6 +3133,27 @@ __global__ void k_rebin(const float *in, float *out, int64_t in_ld, int32_t newl
     }
 }
 
+// observe()'s resampled copy, last step of a run with out_len > 0: bin i of
+// row r = (window sum) / (window width), clipped from above at `clip` in
+// float64 (the reference clips its float64 `out`), cast to float32 or int8
+// (k_clip_cast's int8 rule); an empty window gives NaN (np.nanmean).
+__global__ void k_out_finalize(const double *acc, const int64_t *lo, const int64_t *hi, double step, void *out,
+                               int64_t len, int64_t total, float clip, int32_t kind) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = e % len;
+        const double w = lo ? (double)(hi[i] - lo[i]) : step;
+        double v = w > 0.0 ? acc[e] / w : __builtin_nan("");
+        if (v > (double)clip) v = (double)clip;
+        if (kind == PSS_OUT_F32) {
+            ((float *)out)[e] = (float)v;
+        } else {
+            const float f = fminf(fmaxf((float)v, -128.f), 127.f);
+            ((int8_t *)out)[e] = (int8_t)(int)truncf(f);
+        }
+    }
+}
+
 __global__ void k_clip_cast(const float *in, void *out, int64_t count, float clip, int32_t kind) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
          i += (int64_t)gridDim.x * blockDim.x) {
@@ -3898,6 +4034,13 @@ static int validate(const PssPipeline *p) {
                         "filtered transform off the four-step lengths)", (long long)p->nsamp);
     }
     if (p->out_kind != PSS_OUT_NONE && !p->out) return fail(PSS_EINVAL, "out is NULL");
+    if (p->out_kind != PSS_OUT_NONE && p->out_len > 0) {
+        if (!p->out_acc) return fail(PSS_EINVAL, "resampled out needs out_acc");
+        if ((p->out_lo == nullptr) != (p->out_hi == nullptr)) return fail(PSS_EINVAL, "out_lo / out_hi");
+        if (!(p->out_step >= 1.0)) return fail(PSS_EINVAL, "out_step %g < 1", p->out_step);
+        if (!p->out_lo && (p->out_step != floor(p->out_step) || p->out_step * p->out_len > (double)p->nsamp))
+            return fail(PSS_EINVAL, "uniform windows: integer out_step with out_len * out_step <= nsamp");
+    }
     return PSS_OK;
 }
 
@@ -3958,10 +4101,24 @@ int64_t pss_workspace_bytes(int32_t nchan, int64_t nsamp) {
     return ws_layout(nchan, nsamp).total;
 }
 
+static int run_paths(const PssPipeline *p, hipStream_t st);
+
 int pss_run(const PssPipeline *p, void *stream) {
     int rc = validate(p);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
+    const bool windows = p->out_kind != PSS_OUT_NONE && p->out_len > 0;
+    if (windows) HIPCHK(hipMemsetAsync(p->out_acc, 0, (size_t)p->nchan * (size_t)p->out_len * 8, st));
+    rc = run_paths(p, st);
+    if (rc || !windows) return rc;
+    const int64_t total = (int64_t)p->nchan * p->out_len;
+    k_out_finalize<<<stream_grid(total, 1), dim3(256), 0, st>>>(p->out_acc, p->out_lo, p->out_hi, p->out_step,
+                                                                 p->out, p->out_len, total, p->clip, p->out_kind);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+static int run_paths(const PssPipeline *p, hipStream_t st) {
     KP k;
     memset(&k, 0, sizeof(k));
     k.p = *p;

@@ -3,9 +3,12 @@
 observe() decides the resampling branch exactly as the reference (float
 comparisons of unit-converted dt's, telescope.py:94-126), attaches the
 pre-noise ``out`` copy and the radiometer-noise stage to the signal's pending
-pipeline and executes it as one fused device run; the down_sample / rebin
-branches resample the pre-noise copy with their own kernels before the clip
-and cast (telescope.py:140-145).
+pipeline and executes it as one fused device run.  On the down_sample /
+rebin branches the run itself produces the resampled, clipped and cast
+``out`` (telescope.py:108-125, 140-145): its epilogue adds every pre-noise
+sample into float64 window sums and one small kernel divides, clips and casts
+them (PssPipeline.out_len) -- no full-resolution copy, no separate resampling
+or clip pass.
 """
 import numpy as np
 import torch
@@ -106,34 +109,25 @@ class Telescope(object):
             out = torch.empty((rows, ncols), dtype=odt, device=dev)
             pend.out = {"kind": okind, "tensor": out, "clip": clip}
         elif ret_resampsig:
-            pre = torch.empty((rows, ncols), dtype=torch.float32, device=dev)
-            pend.out = {"kind": _lib.OUT_F32, "tensor": pre, "clip": float("inf")}
-        if noise:
-            rcvr.radiometer_noise(signal, pulsar, gain=self.gain, Tsys=self.Tsys)
-        signal._flush()
-        if ret_resampsig and kind != "copy":
             if kind == "down":
+                # telescope.py:108-114 (down_sample: reshape(-1, fact).mean)
                 new_Nt = int(signal.nsamp // arg)
                 if ncols % arg or ncols // arg != new_Nt:
                     raise ValueError("could not broadcast input array from shape (%d,) into shape (%d,)"
                                      % (ncols // max(arg, 1), new_Nt))
-                res = torch.empty((rows, new_Nt), dtype=torch.float32, device=dev)
-                rc = _lib.lib().pss_down_sample(_engine.ptr(pre), _engine.ptr(res), rows, ncols,
-                                                pre.stride(0), int(arg), _engine.stream_ptr())
-                _lib.check(rc, "observe/down_sample")
+                win = {"len": new_Nt, "lo": None, "hi": None, "step": float(arg)}
             else:
+                # telescope.py:116-125 (rebin: ceil-edged windows, nanmean)
                 new_Nt = int(arg)
                 lo, hi = rebin_edges(ncols, new_Nt)
-                dlo, dhi = _engine.to_dev(lo), _engine.to_dev(hi)
-                res = torch.empty((rows, new_Nt), dtype=torch.float32, device=dev)
-                rc = _lib.lib().pss_rebin(_engine.ptr(pre), _engine.ptr(res), rows, ncols,
-                                          pre.stride(0), new_Nt, _engine.ptr(dlo), _engine.ptr(dhi),
-                                          _engine.stream_ptr())
-                _lib.check(rc, "observe/rebin")
+                step = float(np.linspace(0, ncols, new_Nt, endpoint=False)[1]) if new_Nt > 1 else float(ncols)
+                win = {"len": new_Nt, "lo": _engine.to_dev(lo), "hi": _engine.to_dev(hi), "step": step}
             out = torch.empty((rows, new_Nt), dtype=odt, device=dev)
-            rc = _lib.lib().pss_clip_cast(_engine.ptr(res), _engine.ptr(out), res.numel(), clip, okind,
-                                          _engine.stream_ptr())
-            _lib.check(rc, "observe/clip")
+            win["acc"] = torch.empty((rows, new_Nt), dtype=torch.float64, device=dev)
+            pend.out = {"kind": okind, "tensor": out, "clip": clip, "windows": win}
+        if noise:
+            rcvr.radiometer_noise(signal, pulsar, gain=self.gain, Tsys=self.Tsys)
+        signal._flush()
         if ret_resampsig:
             # the returned copy is a read-out of the data: a null() whose
             # channel-0 maximum was not unique raises here, as the reference's

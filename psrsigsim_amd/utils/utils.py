@@ -73,17 +73,13 @@ def down_sample(ar, fact):
 
 
 def rebin_edges(size, newlen):
-    """Integer windows [lo_i, hi_i) of utils.py:77-89."""
+    """Integer windows [lo_i, hi_i) of utils.py:77-89 -- the same float64
+    operations as the reference's per-bin loop (ceil(lbin), ceil(lbin +
+    stride) clipped to the size), elementwise over the bins."""
     newBins = np.linspace(0, size, newlen, endpoint=False)
     stride = newBins[1] - newBins[0]
-    lo = np.empty(newlen, dtype=np.int64)
-    hi = np.empty(newlen, dtype=np.int64)
-    for ii, lbin in enumerate(newBins):
-        rbin = int(np.ceil(lbin + stride))
-        if rbin > size:
-            rbin = size
-        lo[ii] = int(np.ceil(lbin))
-        hi[ii] = rbin
+    hi = np.minimum(np.ceil(newBins + stride), size).astype(np.int64)
+    lo = np.ceil(newBins).astype(np.int64)
     return lo, hi
 
 

@@ -51,12 +51,14 @@ def test_baseband_golden_exact(tag, hip_lib):
         ISM().disperse(sig, dm)
 
 
-@pytest.mark.parametrize("N", [4096, 51200, 1 << 16, 100002, 20480, 1 << 22])
+@pytest.mark.parametrize("N", [4096, 51200, 1 << 16, 100002, 20480, 1 << 22, 1 << 23, 1 << 24, 196608, 3125000])
 def test_filter_rows_vs_numpy(N, hip_lib):
     """The transfer-function run against numpy irfft(rfft(x) H) in float64:
     single pass (4096), the pair four-step with H in the row pass (2^16,
-    2^22; the mixed-radix 10 x 2048 split at 20480), Bluestein (51200,
-    100002)."""
+    2^22; 8192-point rows at 2^23 = 1024 x 8192 and 2^24 = 2048 x 8192; the
+    mixed-radix 10 x 2048 split at 20480 and 24 x 8192 at 196608; the radix-5
+    1250 x 2500 split at 3 125 000), Bluestein (51200, 100002).  (ADVICE r04:
+    every row-pass instantiation the htab runs can take.)"""
     import torch
     from psrsigsim_amd import _engine
     rng = np.random.default_rng(N)

@@ -3,7 +3,10 @@ item 8): a C3-geometry run -- global channels 0..3 of the 2048-channel band,
 2^22 samples, scatter_broaden(convolve) + disperse(100) + delayed null(0.1)
 + Arecibo radiometer noise, observe() without a returned copy -- so
 k_pairA_fast / k_pair_row / k_pairC_fast / k_null_fix_list run with their
-own Philox draws, not injected ones.  The draws are then recovered with
+own Philox draws, not injected ones.  And the C5 geometry (VERDICT r04 item
+3): global channels 0..3 of the 8192-channel band, 2^24 samples, DM 500,
+delayed null(0.1), noise -- k_pairA_wave (pulse draws keyed in quarter-row
+blocks, pss::pulse_draw), k_pair_row_seq, k_pairC_fast32, k_null_fix_list.  The draws are then recovered with
 pss_chi2_fill (the same counter-based keys: seed, call id, purpose, global
 channel, sample) and replayed through the CPU oracle in the reference's
 draw order (pulses, null pulse choice, box values, replacements, noise).
@@ -65,21 +68,28 @@ class _PhiloxReplay(object):
         return a
 
 
-def test_fast_path_c3_channels_vs_oracle(hip_lib):
+# (name, log2 N, band channels, scatter_broaden(convolve), DM)
+GEOMS = {"c3": (22, 2048, True, 100), "c5": (24, 8192, False, 500)}
+
+
+@pytest.mark.parametrize("geom", sorted(GEOMS))
+def test_fast_path_channels_vs_oracle(geom, hip_lib):
     import psrsigsim_amd as pss
     from psrsigsim_amd import _engine
     from psrsigsim_amd.signal import FilterBankSignal
     from psrsigsim_amd.pulsar import Pulsar, GaussProfile
     from psrsigsim_amd.ism import ISM
     from psrsigsim_amd.telescope import telescope as T
-    N, C, seed = 1 << 22, 4, 0x5EED0003
+    log2n, band, scatter, dm = GEOMS[geom]
+    N, C, seed = 1 << log2n, 4, 0x5EED0003 + log2n
     pss.seed(seed)
-    sig = FilterBankSignal(1400, 400, Nsubband=2048, fold=False, shard=(0, C))
+    sig = FilterBankSignal(1400, 400, Nsubband=band, fold=False, shard=(0, C))
     psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
     ism = ISM()
-    ism.scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
+    if scatter:
+        ism.scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
     psr.make_pulses(sig, tobs=N * 20.48e-6)                 # call 1
-    ism.disperse(sig, 100)
+    ism.disperse(sig, dm)
     psr.null(sig, 0.1)                                      # call 2
     T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True)   # call 3 (no copy: fast epilogue)
     got = sig.data.cpu().numpy().astype(np.float64)
@@ -88,15 +98,15 @@ def test_fast_path_c3_channels_vs_oracle(hip_lib):
     npulse = int(np.round(nsub * 0.1))
     pulses = _engine.host_rng(2).choice(nsub, npulse, replace=False)
     nph = int(psr._nph(sig))
-    gen = _fill(C, 0, N, 1.0, seed, 1, P_PULSE)
+    gen = _fill(C, 0, N, 1.0, seed, 1, P_PULSE)      # (2^24: the quarter-row keying, pss::pulse_draw)
     rep = _fill(C, 0, N, 1.0, seed, 2, P_REP)
     noise = _fill(C, 0, N, 1.0, seed, 3, P_NOISE)
     boxrows = _fill(npulse, 0, nph, 100.0, seed, 2, P_BOX)   # row = rank in the choice list, column = bin
-    case = dict(sig=dict(fcent=1400, bw=400, nchan=2048, fold=False, chans=(0, C)),
-                psr=dict(period=0.005, Smean=1.0, prof=("gauss", 0.5, 0.05, 1)),
-                ops=[("scatter_conv", 1e-4, 1400, None), ("make_pulses", N * 20.48e-6, "pulses"),
-                     ("disperse", 100, "disperse"), ("null", 0.1, "null"),
-                     ("observe", "Arecibo", "Lband_PUPPI", True, "noise")])
+    ops = [("scatter_conv", 1e-4, 1400, None)] if scatter else []
+    ops += [("make_pulses", N * 20.48e-6, "pulses"), ("disperse", dm, "disperse"), ("null", 0.1, "null"),
+            ("observe", "Arecibo", "Lband_PUPPI", True, "noise")]
+    case = dict(sig=dict(fcent=1400, bw=400, nchan=band, fold=False, chans=(0, C)),
+                psr=dict(period=0.005, Smean=1.0, prof=("gauss", 0.5, 0.05, 1)), ops=ops)
     d = _PhiloxReplay(gen, pulses, [boxrows[r] for r in range(npulse)], rep, noise)
     A, inj = replay.oracle_exec(case, d)
     assert not d.queue, "draws left over: the oracle's call order diverged"

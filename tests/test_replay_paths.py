@@ -20,6 +20,9 @@ def test_packed64_lengths():
     assert replay.packed64(10006, c)            # Bluestein
     assert not replay.packed64(8192, c)         # single-workgroup kernel: fp32
     assert not replay.packed64(4096, c)
+    assert not replay.packed64(64, c)           # the smallest single-workgroup length
+    assert replay.packed64(32, c)               # 2^m < 64: direct DFT, refined
+    assert replay.packed64(16, c)
     assert not replay.packed64(10007, c)        # odd: shift_t only
     assert not replay.packed64((1 << 17) + 2, c)
     assert not replay.packed64(30720, _case(tail=True))
@@ -29,3 +32,6 @@ def test_packed_bounds_tightened():
     assert replay.AMBIG_MAX_FRAC["packed"] <= 2e-3
     assert replay.FLIP_MAX_FRAC["packed"] <= 1e-5
     assert replay.AMBIG_MAX_FRAC["table"] <= 2e-3
+    # fp32-decided lengths: ~10x the measured band (3.05e-5) and no flips
+    assert replay.AMBIG_MAX_FRAC["packed_f32"] <= 3e-4
+    assert replay.FLIP_MAX_FRAC["packed_f32"] <= 1e-5
