@@ -175,9 +175,33 @@ if os.environ.get("PSS_NO_MALLOPT") is None:
     _tune_host_malloc()
 
 
+_HOST_THREADS = []
+
+
 def host_threads():
-    n = os.environ.get("PSS_HOST_THREADS")
-    return max(1, int(n)) if n else max(1, min(8, os.cpu_count() or 1))
+    if not _HOST_THREADS:
+        n = os.environ.get("PSS_HOST_THREADS")
+        _HOST_THREADS.append(max(1, int(n)) if n else max(1, min(8, os.cpu_count() or 1)))
+    return _HOST_THREADS[0]
+
+
+_POOL = []
+
+
+def host_rows(rows, fn, min_rows=128):
+    """fn(a, b) over row blocks [a, b) of ``rows`` rows on host_threads()
+    threads (numpy / pocketfft release the GIL in their array loops); the
+    blocks are disjoint, so the result does not depend on the split."""
+    nt = min(host_threads(), max(1, rows // min_rows))
+    if nt <= 1:
+        fn(0, rows)
+        return
+    if not _POOL:
+        from concurrent.futures import ThreadPoolExecutor
+        _POOL.append(ThreadPoolExecutor(max_workers=host_threads(), thread_name_prefix="pss-plan"))
+    futs = [_POOL[0].submit(fn, rows * t // nt, rows * (t + 1) // nt) for t in range(nt)]
+    for f in futs:
+        f.result()
 
 
 def _dptr(a):

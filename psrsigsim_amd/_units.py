@@ -98,29 +98,41 @@ UNITS = {
 _TOK = re.compile(r"\s*([A-Za-z]+)\s*(?:(?:\^|\*\*)\s*(-?[0-9.]+))?\s*")
 
 
+_PARSED = {}
+
+
 def as_unit(x):
     if isinstance(x, Unit):
         return x
     if isinstance(x, str):
-        s = x.strip()
-        if s in UNITS:
-            return UNITS[s]
-        out, op, pos = UNITS[""], "*", 0
-        while pos < len(s):
-            m = _TOK.match(s, pos)
-            if not m or m.group(1) not in UNITS:
-                raise ValueError("cannot parse unit %r" % x)
-            u = UNITS[m.group(1)] ** (float(m.group(2)) if m.group(2) else 1.0)
-            out = out * u if op == "*" else out / u
-            pos = m.end()
-            if pos < len(s):
-                op = s[pos]
-                if op not in "*/":
-                    raise ValueError("cannot parse unit %r" % x)
-                pos += 1
-        out.name = s
-        return out
+        u = UNITS.get(x)
+        if u is None:
+            u = _PARSED.get(x)
+        if u is None:
+            u = _PARSED[x] = _parse_unit(x)      # compound strings parsed once per process
+        return u
     raise TypeError("not a unit: %r" % (x,))
+
+
+def _parse_unit(x):
+    s = x.strip()
+    if s in UNITS:
+        return UNITS[s]
+    out, op, pos = UNITS[""], "*", 0
+    while pos < len(s):
+        m = _TOK.match(s, pos)
+        if not m or m.group(1) not in UNITS:
+            raise ValueError("cannot parse unit %r" % x)
+        u = UNITS[m.group(1)] ** (float(m.group(2)) if m.group(2) else 1.0)
+        out = out * u if op == "*" else out / u
+        pos = m.end()
+        if pos < len(s):
+            op = s[pos]
+            if op not in "*/":
+                raise ValueError("cannot parse unit %r" % x)
+            pos += 1
+    out.name = s
+    return out
 
 
 class Quantity(object):
@@ -128,9 +140,13 @@ class Quantity(object):
     __array_priority__ = 1000
 
     def __init__(self, value, unit=""):
-        if isinstance(value, Quantity):
-            value = value.to(unit).value if unit != "" else value.value
-        self._value = np.asarray(value, dtype=float) if np.ndim(value) else float(value)
+        t = type(value)
+        if t is float or t is int:
+            self._value = float(value)        # (the common scalar case, without numpy)
+        else:
+            if isinstance(value, Quantity):
+                value = value.to(unit).value if unit != "" else value.value
+            self._value = np.asarray(value, dtype=float) if np.ndim(value) else float(value)
         self.unit = as_unit(unit)
 
     # -- access --------------------------------------------------------

@@ -495,37 +495,6 @@ __device__ __forceinline__ void draw4(const Rng &g, int64_t n0, uint32_t c, floa
     }
 }
 
-// Search-mode chi2(1) pulse draw of sample n in a row of N samples (P_PULSE,
-// df = 1; `scale` = draw_norm folded into the sampler).  Keying: Philox block
-// n >> 2 holds samples 4 (n >> 2) .. + 3 (the LDS-staged fast pass A draws a
-// block per 4 consecutive samples of a row), except for rows of N >= 2^24,
-// N % 4 == 0 (C5's 2048 x 8192 split): there block m < N/4 holds samples
-// m + e N/4 (e < 4, its four draws in order) -- the rows n1, n1 + N1/4,
-// n1 + N1/2, n1 + 3 N1/4 of one four-step column, so a column's values are
-// drawn where the column is transformed (passA_wave: no cross-wave
-// transpose of the generated samples).  Every path draws through this rule
-// (or the same blocks), so results do not depend on the path.
-__host__ __device__ constexpr bool pulse_quarter(int64_t N) { return (N & 3) == 0 && N >= (int64_t(1) << 24); }
-__device__ __forceinline__ void pulse_block(int64_t n, int64_t N, uint32_t &m, uint32_t &tag, uint32_t &e) {
-    uint64_t mm;
-    if (pulse_quarter(N)) {
-        const uint64_t Q = (uint64_t)N >> 2;
-        e = (uint32_t)((uint64_t)n / Q);
-        mm = (uint64_t)n - (uint64_t)e * Q;
-    } else {
-        mm = (uint64_t)n >> 2;
-        e = (uint32_t)(n & 3);
-    }
-    m = (uint32_t)mm;
-    tag = (uint32_t)(mm >> 32);
-}
-__device__ __forceinline__ float pulse_draw(const Rng &g, int64_t n, int64_t N, uint32_t c, float scale) {
-    uint32_t m, tag, e;
-    pulse_block(n, N, m, tag, e);
-    const float4 q = chi2_1x4(g.bits(m, c, tag), scale);
-    return e == 0u ? q.x : (e == 1u ? q.y : (e == 2u ? q.z : q.w));
-}
-
 // Interval index and fraction of sample n's pulse phase (shared by every
 // channel: only the coefficient row differs).
 __device__ __forceinline__ void pchip_locate(const KP &k, int64_t n, uint32_t &iv, float &u) {
@@ -670,14 +639,10 @@ __device__ __forceinline__ void source4(const KP &k, int r, int64_t n0, int cnt,
             } else if (p.gen_df == 1.0f) {
                 // chi2(1) draws with draw_norm folded into the sampler (as the
                 // fast pass A draws them: bitwise the same values)
+                // (Philox block n >> 2 holds samples 4 (n >> 2) .. + 3 at every N)
                 Rng g(p.seed, p.call_gen, P_PULSE);
-                if (pulse_quarter(k.N)) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) x[i] = (i < cnt) ? pulse_draw(g, n0 + i, k.N, c, p.draw_norm) : 0.f;
-                } else {
-                    const float4 q = chi2_1x4(g.bits((uint32_t)(n0 >> 2), c, (uint32_t)(n0 >> 34)), p.draw_norm);
-                    x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
-                }
+                const float4 q = chi2_1x4(g.bits((uint32_t)(n0 >> 2), c, (uint32_t)(n0 >> 34)), p.draw_norm);
+                x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
                 dn = 1.0f;                                   // (x * 1 is exact)
             } else {
                 Rng g(p.seed, p.call_gen, P_PULSE);
@@ -1815,7 +1780,7 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             // edges): the multiply the sample needs anyway zeroes it, no select
             const float dna = hasa ? p.draw_norm : 0.f, dnb = hasb ? p.draw_norm : 0.f;
             // item = 4 consecutive samples n .. n + 3 of row n1 (Philox block
-            // n >> 2: pulse_draw's keying below 2^24), phases by a unit walk
+            // n >> 2, at every N), phases by a unit walk
             uint32_t dlo;
             uint64_t dhi;
             phase_delta(p, dlo, dhi);
@@ -1943,143 +1908,6 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
             }
             FF::template store<RFL>(v, lds, tid);
         }
-        __syncthreads();
-        spill_block(k, lds, tid, pr, n20);
-    }
-
-    // ------------------------------------------------------------------
-    // Wave-local fast pass A (the wave-column geometries: C3's 1024 x 4096
-    // and C5's 2048 x 8192 splits).  Wave wv owns column n2 = n20 + wv and
-    // lane l its rows l + 64 q (q < E) -- exactly the first Stockham stage's
-    // inputs -- and draws them itself: with pulse_draw's keying the Philox
-    // block m = (l + 64 q') N2 + n2 (q' < E/4) holds rows q' + (E/4) e, so the
-    // values go straight into the registers (no LDS staging, no transpose and
-    // no workgroup barrier before the FFT); the phases walk the column in
-    // strides of 64 N2 samples.  Bitwise the values of passA<true>.
-    // ------------------------------------------------------------------
-    static constexpr bool kWaveA = kWaveCols && kMergeTw && kItemsExact && RF0 == 16 && (N1 % 64 == 0);
-    // The wave's column: profile x draws straight into the first stage's
-    // input registers (register ib R0 + q holds row lane + 64 ib + LR q,
-    // Fft::load's mapping; a Philox block covers rows r + e N1/4 = registers
-    // + 4 e, R0 = 16: N1/4 = 4 LR), phases by a walk in strides of LR rows.
-    template <bool SHARED>
-    __device__ static __forceinline__ void wave_column(const KP &k, cf (&v)[E], const float4 (*ptab)[kFastNint],
-                                                       int lane, uint32_t n2, uint32_t ca, float dna, float dnb) {
-        static_assert(RF0 == 16, "wave-local pass A: radix-16 first stage");
-        constexpr int LR = N1 / RF0;
-        const PssPipeline &p = k.p;
-        const uint32_t N2 = (uint32_t)k.N2, cb = ca + 1u;
-        const Rng g(p.seed, p.call_gen, P_PULSE);
-        uint32_t dlo;
-        uint64_t dhi;
-        phase_delta_n(p, (uint64_t)LR * (uint64_t)N2, dlo, dhi);
-        const uint32_t M = p.knot_m;
-#pragma unroll
-        for (int ib = 0; ib < E / RF0; ++ib) {
-            // profile values of the rows, in the register of their row
-            PhaseWalk w;
-            w.start(p, (uint32_t)(lane + 64 * ib) * N2 + n2);   // N <= 2^24
-#pragma unroll
-            for (int q = 0; q < RF0; ++q) {
-                uint32_t iv;
-                float u;
-                if (q) w.step(dlo, dhi, M);
-                w.get_full(iv, u);       // fast_source(): nint == knot_m
-                const float4 A = ptab[0][iv];
-                const float pa = fmaf(fmaf(fmaf(A.x, u, A.y), u, A.z), u, A.w);
-                float pb = pa;
-                if constexpr (!SHARED) {
-                    const float4 Bc = ptab[1][iv];
-                    pb = fmaf(fmaf(fmaf(Bc.x, u, Bc.y), u, Bc.z), u, Bc.w);
-                }
-                v[ib * RF0 + q] = make_float2(pa, pb);
-            }
-            // times the draws: block of row lane + 64 ib + LR q (q < 4)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t m = (uint32_t)(lane + 64 * ib + LR * q) * N2 + n2;
-                const float4 qa = chi2_1x4(g.bits(m, ca, 0u), dna);
-                const float4 qb = chi2_1x4(g.bits(m, cb, 0u), dnb);
-                const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    cf &x = v[ib * RF0 + q + 4 * e];
-                    x = make_float2(x.x * va[e], x.y * vb[e]);
-                }
-            }
-        }
-    }
-    // The column FFT's last stage (radix RFL at Ns = N1 / RFL) with the
-    // four-step twiddle W_N^{n2 k1} merged in (passA's merged stage): output
-    // m of butterfly jj is k1 = jj + Ns m; phases in exact 32-bit fixed point.
-    __device__ static __forceinline__ void last_stage_tw(const KP &k, cf (&v)[E], int lane, uint32_t n2) {
-        constexpr int NsL = N1 / RFL;
-        constexpr int LG1 = __builtin_ctz((unsigned)N1);
-        const int LGN = __builtin_ctzll((unsigned long long)k.N);        // N = 2^LGN here
-        const uint32_t A = n2 << (32 - LGN);                              // n2 / N (2^-32 rev)
-        cf U[RFL];
-#pragma unroll
-        for (int m = 1; m < RFL; ++m) U[m] = expi_rev(-fix32_to_rev(A * (uint32_t)(NsL * m)));
-#pragma unroll
-        for (int ib = 0; ib < E / RFL; ++ib) {
-            const uint32_t jj = (uint32_t)(lane + 64 * ib);              // < NsL
-            const uint32_t X0 = jj * A, S = jj << (32 - LG1);
-            cf *a = v + ib * RFL;
-#pragma unroll
-            for (int q = 0; q < RFL; ++q) a[q] = cmul(a[q], expi_rev(-fix32_to_rev(X0 + (uint32_t)q * S)));
-            dft<RFL, false>(a);
-#pragma unroll
-            for (int m = 1; m < RFL; ++m) a[m] = cmul(a[m], U[m]);
-        }
-    }
-    // Setup shared by the wave-local pass A kernels: block, pair, PCHIP rows
-    // of the pair staged in LDS (and tw16 filled); ends with the barrier.
-    template <bool SHARED>
-    __device__ static __forceinline__ void wave_setup(const KP &k, float4 (*ptab)[kFastNint], cf *tw16, int tid,
-                                                      int &pr, int64_t &n20, uint32_t &ca, float &dna, float &dnb) {
-        tw16_fill(tw16, tid, T);
-        int cbx;
-        xcd_block(cbx, pr);
-        const int ra = 2 * pr - k.poff, rb = ra + 1;
-        const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
-        n20 = (int64_t)cbx * B;
-        const PssPipeline &p = k.p;
-        ca = (uint32_t)(p.chan0 + ra);
-        const int pra = (p.prof_rows == 1) ? 0 : (int)ca - p.prof_row0;
-        const int prb = (p.prof_rows == 1) ? 0 : (int)ca + 1 - p.prof_row0;
-        const int nint = p.nint, last = p.prof_rows - 1;
-        const int rowa = min(max(pra, 0), last), rowb = min(max(prb, 0), last);
-        const float4 *prof = reinterpret_cast<const float4 *>(p.prof);
-        for (int i = tid; i < nint; i += T) {
-            ptab[0][i] = prof[(int64_t)rowa * nint + i];
-            if constexpr (!SHARED) ptab[1][i] = prof[(int64_t)rowb * nint + i];
-        }
-        // draw_norm, or 0 for a pair's missing channel (shard / band edges)
-        dna = hasa ? p.draw_norm : 0.f;
-        dnb = hasb ? p.draw_norm : 0.f;
-        __syncthreads();                // the tables (tw16 is first read in the FFT's second stage)
-    }
-    template <bool SHARED>
-    __device__ static void passA_wave(const KP &k) {
-        static_assert(kWaveA, "wave-local pass A: one wave per column");
-        __shared__ __align__(128) cf lds[B * LdsC::RS];   // (128-B aligned: the FFT's byte-address exchanges)
-        __shared__ cf tw16[kTw16Size];
-        __shared__ float4 ptab[SHARED ? 1 : 2][kFastNint];
-        const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-        int pr;
-        int64_t n20;
-        uint32_t ca;
-        float dna, dnb;
-        wave_setup<SHARED>(k, ptab, tw16, tid, pr, n20, ca, dna, dnb);
-        const uint32_t n2 = (uint32_t)(n20 + wv);
-        cf v[E];
-        wave_column<SHARED>(k, v, ptab, lane, n2, ca, dna, dnb);
-        // column FFT (wave-local) with the four-step twiddle merged into the
-        // last stage: as passA
-        cf *wl = lds + wv * LdsC::RS;
-        FW::template run_head_tw<false, 1, F...>(v, wl, lane, tw16);
-        last_stage_tw(k, v, lane, n2);
-        FW::template store<RFL>(v, wl, lane);
         __syncthreads();
         spill_block(k, lds, tid, pr, n20);
     }
@@ -2538,8 +2366,6 @@ template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairA(KP k) { C::template passA<false>(k); }
 template <typename C, int T, bool SHARED>
 __global__ __launch_bounds__(T) void k_pairA_fast(KP k) { C::template passA<true, SHARED>(k); }
-template <typename C, int T, bool SHARED>
-__global__ __launch_bounds__(T) void k_pairA_wave(KP k) { C::template passA_wave<SHARED>(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairC(KP k) { C::passC(k); }
 template <typename C, int T>
@@ -3240,13 +3066,7 @@ __global__ void k_chi2_fill(float *out, int64_t n, int32_t chan0, float df, uint
          it += (int64_t)gridDim.x * blockDim.x) {
         const int64_t n0 = it << 2;
         float x[4];
-        if (purpose == P_PULSE && df == 1.0f && (n & 3) == 0) {
-            // the search pulses' layout (pulse_draw: rows of n samples)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) x[i] = pulse_draw(g, n0 + i, n, (uint32_t)(chan0 + r), 1.0f);
-        } else {
-            draw4(g, n0, (uint32_t)(chan0 + r), df, x);
-        }
+        draw4(g, n0, (uint32_t)(chan0 + r), df, x);
         for (int i = 0; i < 4 && n0 + i < n; ++i) out[(int64_t)r * n + n0 + i] = x[i];
     }
 }
@@ -3296,6 +3116,8 @@ using C2kI = RList<8, 16, 16>;
 using C4k = RList<16, 16, 16>;
 using C8kF = RList<16, 8, 8, 8>;
 using C8kI = RList<8, 8, 8, 16>;
+using C16kF = RList<16, 16, 8, 8>;
+using C16kI = RList<8, 8, 16, 16>;
 
 // ---------------------------------------------------------------------------
 // workspace layout (every region 256-B aligned)
@@ -3592,7 +3414,7 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
     if (k.p.null_mode == PSS_NULL_DELAYED) {
         // the mask table's position arithmetic is for N = 2^m (validate()
         // sends delayed nulls of other lengths to the direct path)
-        if constexpr ((N1 & (N1 - 1)) == 0) {
+        if constexpr ((N1 & (N1 - 1)) == 0 && N2 <= 8192) {
             // With the data in the FFT and the fast passes, nothing reads the
             // table before the null fix-up: build it on a side stream next to
             // pass A (its dozen small launches then cost no time on the main
@@ -3611,7 +3433,8 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
                 k.mask_ready = ss->ev[31];
             }
         } else {
-            return fail(PSS_EUNSUPPORTED, "delayed null on the mixed-radix four-step (N=%lld)", (long long)k.N);
+            return fail(PSS_EUNSUPPORTED, "delayed null on the mixed-radix or 16384-row four-step (N=%lld)",
+                        (long long)k.N);
         }
     }
     if (!k.p.data_in_fft) {
@@ -3652,21 +3475,8 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     if (launched) {
     } else if constexpr (PC::kItemsExact) {
         if (fast_source(k.p)) {
-            // C5's split (quarter-keyed pulses, N >= 2^24): the wave-local
-            // kernel; otherwise the LDS-staged passA<true>
-            bool wave = false;
-            if constexpr (PC::kWaveA) wave = pulse_quarter(k.N);
-            if (wave) {
-                if constexpr (PC::kWaveA) {
-                    if (k.p.prof_rows == 1) k_pairA_wave<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
-                    else k_pairA_wave<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
-                }
-            } else if (!pulse_quarter(k.N)) {
-                if (k.p.prof_rows == 1) k_pairA_fast<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
-                else k_pairA_fast<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
-            } else {
-                k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
-            }
+            if (k.p.prof_rows == 1) k_pairA_fast<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
+            else k_pairA_fast<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
         } else {
             k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
         }
@@ -3676,7 +3486,16 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     tk_end(st);
     LAUNCHCHK();
     tk_begin(TK_ROW, st);
-    if (k.p.htab) {
+    if constexpr (N2 > 8192) {
+        // 16384-point rows (C5's 1024 x 16384 split): one row at a time
+        // (PairRowsSeq); no transfer function / tail variant (run_fourstep
+        // keeps those runs on the 2048 x 8192 split)
+        if (k.p.htab || k.p.tail_a) return fail(PSS_EUNSUPPORTED, "%d-point rows: no transfer function", N2);
+        constexpr int TS = N2 / 16;                  // 16 values of each row per thread
+        using PRS = PairRowsSeq<N2, TS, RF, RI>;
+        k_pair_row_seq<PRS, TS, false><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2 - 1)), dim3(TS), 0, st>>>(k);
+        k_pair_row_seq<PRS, TS, true><<<dim3((unsigned)k.npairs, 1u), dim3(TS), 0, st>>>(k);
+    } else if (k.p.htab) {
         k_pair_row<PR, TR, false, true><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
     } else if (k.p.tail_a) {
         k_pair_row<PR, TR, true><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
@@ -3742,9 +3561,19 @@ static int run_fourstep(KP &k, hipStream_t st, const float *mask_row) {
         return launch_pair<1024, 8, 512, C1kF, C1kF, 8192, 1024, C8kF, C8kI, 512>(k, st, mask_row);
     }
     if (N == (1 << 24)) {
-        // C5 rows: 2048 x 8192.  Pass A: 8 columns, one wave per 2048-point
-        // column (wave-local FFTs, 32 values per lane; 64-B spill segments);
-        // pass C: 16-column register-resident blocks (passC_fast32)
+        if (k.p.null_mode != PSS_NULL_DELAYED && !k.p.htab && !k.p.tail_a) {
+            // C5: 1024 x 16384 -- C3's column kernels (1024-point columns:
+            // pass A two workgroups per CU, pass C 16-column blocks) and a
+            // one-row-at-a-time 16384-point row pass (PairRowsSeq, 1024
+            // threads, 133 KB of LDS)
+            k.N2 = 16384;
+            k.N1 = 1024;
+            return launch_pair<1024, 8, 512, C1kF, C1kF, 16384, 1024, C16kF, C16kI, 1024, kBC, kTC>(k, st, mask_row);
+        }
+        // with a delayed null (the mask table's row engine holds a pair of
+        // rows), a transfer function or the tail: 2048 x 8192.  Pass A: the
+        // LDS-staged fast kernel on 2048-point columns; pass C: 16-column
+        // register-resident blocks (passC_fast32)
         k.N2 = 8192;
         k.N1 = 2048;
         return launch_pair<2048, 8, 512, C2kF, C2kF, 8192, 1024, C8kF, C8kI, 512, 8, 1024>(k, st, mask_row);

@@ -7,7 +7,6 @@ delay stages run as ONE forward/inverse FFT pass on the GPU (the reference runs
 one rfft/irfft pair per channel per call: ism.py:57-60, 136-139, 203-206).
 """
 import numpy as np
-from scipy import fft as _sp_fft
 from scipy.signal import fftconvolve as _fftconvolve
 
 from ..utils.constants import DM_K_VALUE, KOLMOGOROV_BETA
@@ -159,20 +158,25 @@ class ISM(object):
     def convolve_profile(self, profiles, convolve_array, width=2048):
         """ism.py:243-288: per row, linear convolution of the sum-normalised
         profile with the sum-normalised kernel, first `width` samples,
-        rescaled by the profile sum."""
+        rescaled by the profile sum.  Row blocks run on host threads (every
+        step is row-wise: numpy and pocketfft release the GIL), so the
+        per-signal planning of a 2048-channel band is not one core's work."""
         prof = np.asarray(profiles, dtype=float)
         kern = np.asarray(convolve_array, dtype=float)
         rows = kern.shape[0]
-        ps = np.sum(prof[:rows], axis=1, keepdims=True)
-        pn = np.where(ps != 0.0, prof[:rows] / np.where(ps != 0.0, ps, 1.0), prof[:rows])
-        ks = np.sum(kern, axis=1, keepdims=True)
-        kn = np.where(ks != 0.0, kern / np.where(ks != 0.0, ks, 1.0), kern)
-        # scipy's FFT convolution batched over rows: bit-identical to the
-        # reference's per-row scipy.signal.convolve(..., method='fft') (the
-        # reference later makes exact float decisions on these values).
-        with _sp_fft.set_workers(_lib.host_threads()):    # pocketfft threads over rows
+
+        def block(a, b):
+            ps = np.sum(prof[a:b], axis=1, keepdims=True)
+            pn = np.where(ps != 0.0, prof[a:b] / np.where(ps != 0.0, ps, 1.0), prof[a:b])
+            ks = np.sum(kern[a:b], axis=1, keepdims=True)
+            kn = np.where(ks != 0.0, kern[a:b] / np.where(ks != 0.0, ks, 1.0), kern[a:b])
+            # scipy's FFT convolution batched over rows: bit-identical to the
+            # reference's per-row scipy.signal.convolve(..., method='fft')
+            # (the reference later makes exact float decisions on these values)
             conv = _fftconvolve(pn, kn, mode='full', axes=1)
-        profiles[:rows, :] = ps * conv[:, :width]
+            profiles[a:b, :] = ps * conv[:, :width]
+
+        _lib.host_rows(rows, block)
         return profiles
 
     def scale_dnu_d(self, dnu_d, nu_i, nu_f, beta=KOLMOGOROV_BETA):

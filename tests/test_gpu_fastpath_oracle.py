@@ -5,8 +5,10 @@ item 8): a C3-geometry run -- global channels 0..3 of the 2048-channel band,
 k_pairA_fast / k_pair_row / k_pairC_fast / k_null_fix_list run with their
 own Philox draws, not injected ones.  And the C5 geometry (VERDICT r04 item
 3): global channels 0..3 of the 8192-channel band, 2^24 samples, DM 500,
-delayed null(0.1), noise -- k_pairA_wave (pulse draws keyed in quarter-row
-blocks, pss::pulse_draw), k_pair_row_seq, k_pairC_fast32, k_null_fix_list.  The draws are then recovered with
+noise -- without a null (BASELINE C5: the 1024 x 16384 split, C3's
+k_pairA_fast / k_pairC_fast and the 16384-point k_pair_row_seq) and with a
+delayed null(0.1) (the 2048 x 8192 split: k_pairA_fast on 2048-point
+columns, the 8192-point k_pair_row_seq, k_pairC_fast32, k_null_fix_list).  The draws are then recovered with
 pss_chi2_fill (the same counter-based keys: seed, call id, purpose, global
 channel, sample) and replayed through the CPU oracle in the reference's
 draw order (pulses, null pulse choice, box values, replacements, noise).
@@ -68,8 +70,9 @@ class _PhiloxReplay(object):
         return a
 
 
-# (name, log2 N, band channels, scatter_broaden(convolve), DM)
-GEOMS = {"c3": (22, 2048, True, 100), "c5": (24, 8192, False, 500)}
+# (name, log2 N, band channels, scatter_broaden(convolve), DM, null)
+GEOMS = {"c3": (22, 2048, True, 100, True), "c5": (24, 8192, False, 500, False),
+         "c5_null": (24, 8192, False, 500, True)}
 
 
 @pytest.mark.parametrize("geom", sorted(GEOMS))
@@ -80,7 +83,7 @@ def test_fast_path_channels_vs_oracle(geom, hip_lib):
     from psrsigsim_amd.pulsar import Pulsar, GaussProfile
     from psrsigsim_amd.ism import ISM
     from psrsigsim_amd.telescope import telescope as T
-    log2n, band, scatter, dm = GEOMS[geom]
+    log2n, band, scatter, dm, null = GEOMS[geom]
     N, C, seed = 1 << log2n, 4, 0x5EED0003 + log2n
     pss.seed(seed)
     sig = FilterBankSignal(1400, 400, Nsubband=band, fold=False, shard=(0, C))
@@ -90,27 +93,35 @@ def test_fast_path_channels_vs_oracle(geom, hip_lib):
         ism.scatter_broaden(sig, 1e-4, 1400, convolve=True, pulsar=psr)
     psr.make_pulses(sig, tobs=N * 20.48e-6)                 # call 1
     ism.disperse(sig, dm)
-    psr.null(sig, 0.1)                                      # call 2
-    T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True)   # call 3 (no copy: fast epilogue)
+    if null:
+        psr.null(sig, 0.1)                                  # call 2
+    T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True)   # call 3 / 2 (no copy: fast epilogue)
     got = sig.data.cpu().numpy().astype(np.float64)
     # the device's draws, recovered by key
-    nsub = int(sig.nsub)
-    npulse = int(np.round(nsub * 0.1))
-    pulses = _engine.host_rng(2).choice(nsub, npulse, replace=False)
-    nph = int(psr._nph(sig))
-    gen = _fill(C, 0, N, 1.0, seed, 1, P_PULSE)      # (2^24: the quarter-row keying, pss::pulse_draw)
-    rep = _fill(C, 0, N, 1.0, seed, 2, P_REP)
-    noise = _fill(C, 0, N, 1.0, seed, 3, P_NOISE)
-    boxrows = _fill(npulse, 0, nph, 100.0, seed, 2, P_BOX)   # row = rank in the choice list, column = bin
+    gen = _fill(C, 0, N, 1.0, seed, 1, P_PULSE)
+    if null:
+        nsub = int(sig.nsub)
+        npulse = int(np.round(nsub * 0.1))
+        pulses = _engine.host_rng(2).choice(nsub, npulse, replace=False)
+        nph = int(psr._nph(sig))
+        rep = _fill(C, 0, N, 1.0, seed, 2, P_REP)
+        boxrows = _fill(npulse, 0, nph, 100.0, seed, 2, P_BOX)   # row = rank in the choice list, column = bin
+    noise = _fill(C, 0, N, 1.0, seed, 3 if null else 2, P_NOISE)
     ops = [("scatter_conv", 1e-4, 1400, None)] if scatter else []
-    ops += [("make_pulses", N * 20.48e-6, "pulses"), ("disperse", dm, "disperse"), ("null", 0.1, "null"),
-            ("observe", "Arecibo", "Lband_PUPPI", True, "noise")]
+    ops += [("make_pulses", N * 20.48e-6, "pulses"), ("disperse", dm, "disperse")]
+    ops += [("null", 0.1, "null")] if null else []
+    ops += [("observe", "Arecibo", "Lband_PUPPI", True, "noise")]
     case = dict(sig=dict(fcent=1400, bw=400, nchan=band, fold=False, chans=(0, C)),
                 psr=dict(period=0.005, Smean=1.0, prof=("gauss", 0.5, 0.05, 1)), ops=ops)
-    d = _PhiloxReplay(gen, pulses, [boxrows[r] for r in range(npulse)], rep, noise)
+    if null:
+        d = _PhiloxReplay(gen, pulses, [boxrows[r] for r in range(npulse)], rep, noise)
+    else:
+        d = _PhiloxReplay(gen, None, [], None, noise)
+        d.queue = [q for q in d.queue if q[0] != "choice"]
     A, inj = replay.oracle_exec(case, d)
     assert not d.queue, "draws left over: the oracle's call order diverged"
     err = replay._err(got, A["data_noise"], inj.get("ambiguous"))
     assert err <= TOL, err
-    amb = inj["ambiguous"]
-    assert amb.mean() <= replay.AMBIG_MAX_FRAC["table"]
+    if null:
+        amb = inj["ambiguous"]
+        assert amb.mean() <= replay.AMBIG_MAX_FRAC["table"]
