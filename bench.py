@@ -187,6 +187,107 @@ def s5_step(pss, nchan_total, shard, plan_group=None):
 
 S5_NSAMP = 3125000
 
+# The reference's only published timings: the
+# dispersion loop's progress line in its tutorials -- disperse stage only,
+# hardware unstated.  (shape, ch-samp/s, source)
+PUBLISHED = {
+    "t1": {"value": 8.8e6, "chans": 126, "nsamp": 97656, "seconds": 1.399, "source": "docs/tutorial_1.rst:178",
+           "stage": "ISM.disperse (search mode, 126 of 128 channels at the 98% progress line)"},
+    "t2": {"value": 1.84e7, "chans": 63, "nsamp": 40960, "seconds": 0.140, "source": "docs/tutorial_2.rst:150",
+           "stage": "ISM.disperse (fold mode, 63 of 64 channels at the 98% progress line)"},
+}
+T1_NSAMP, T2_NSAMP = 97656, 40960
+
+
+def tutorial_signal(workload, nchan_total, shard, plan_group=None):
+    """The tutorials' signals (BASELINE.md section 1's published shapes):
+    t1 = docs/tutorial_1.rst (FilterBankSignal(820, 200, Nsubband=128,
+    fold=False) at the default 0.048828125 MHz, GaussProfile(0.5, 0.05, 1),
+    Pulsar(1 s, 10 Jy), 2 s -> 97 656 samples = 2^3 3 13 313: the Bluestein
+    path; DM 40; GBT 820_GUPPI); t2 = docs/tutorial_2.rst (FilterBankSignal(
+    1500, 800, Nsubband=64, sample_rate=2048 / 10 ms, sublen=60, fold=True),
+    Pulsar(10 ms, 5 mJy, specidx=-1.6, ref_freq=1400), 20 min -> 20 x 2048 =
+    40 960 samples: the mixed-radix 10 x 4096 split; DM 40; GBT
+    Lband_GUPPI).  Returns (signal, pulsar, dm, telescope, system) with the
+    pulses made."""
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+    from psrsigsim_amd.telescope import telescope as T
+    prof = GaussProfile(peak=0.5, width=0.05, amp=1.0)
+    if workload == "t1":
+        sig = FilterBankSignal(820, 200.0, Nsubband=nchan_total, fold=False, shard=shard, plan_group=plan_group)
+        psr = Pulsar(1.0, 10.0, profiles=prof, name="J0000+0000")
+        psr.make_pulses(sig, tobs=2.0)
+        return sig, psr, 40.0, T.GBT(), "820_GUPPI"
+    sig = FilterBankSignal(1500, 800.0, Nsubband=nchan_total, sample_rate=(1.0 / 0.010) * 2048 * 10 ** -6,
+                           sublen=60.0, fold=True, shard=shard, plan_group=plan_group)
+    psr = Pulsar(0.010, 0.005, profiles=prof, name="J0000+0000", specidx=-1.6, ref_freq=1400.0)
+    psr.make_pulses(sig, tobs=60.0 * 20)
+    return sig, psr, 40.0, T.GBT(), "Lband_GUPPI"
+
+
+def tutorial_step(pss, workload, nchan_total, shard, plan_group=None):
+    """One pass of the tutorial's pipeline: make_pulses, disperse, observe
+    with radiometer noise."""
+    from psrsigsim_amd.ism import ISM
+    sig, psr, dm, tel, system = tutorial_signal(workload, nchan_total, shard, plan_group)
+    ISM().disperse(sig, dm)
+    tel.observe(sig, psr, system=system, noise=True)
+    return sig
+
+
+def tutorial_disperse_only(pss, workload, nchan, steps):
+    """The published stage alone: ISM.disperse on a materialised pulse signal
+    of the tutorial's shape (device-resident, the pulses made and read out
+    before the clock starts), K timed calls -> ch-samp/s."""
+    import torch
+    from psrsigsim_amd.ism import ISM
+    sigs = []
+    for _ in range(steps + 1):
+        sig, psr, dm, _, _ = tutorial_signal(workload, nchan, (0, nchan))
+        _ = sig.data                                # pulses materialised (not timed)
+        sigs.append((sig, dm))
+    sig, dm = sigs[0]
+    ISM().disperse(sig, dm)                         # warm-up
+    _ = sig.data
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for sig, dm in sigs[1:]:
+        ISM().disperse(sig, dm)
+        _ = sig.data                                # the delay stage runs here
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    n = int(sigs[0][0].data.shape[1])
+    return nchan * n / dt, dt
+
+
+def cpu_tutorial(workload, nchan):
+    """The oracle on the tutorial shape: the disperse stage alone (what the
+    published line times: per-channel rfft -> ramp -> irfft in float64) and
+    the whole pipeline, single process."""
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    from oracle import pss_cpu as O
+    d = O.LegacyDraws(1776)
+    if workload == "t1":
+        sig = O.Signal(820, 200.0, nchan=nchan, fold=False)
+        psr = O.Pulsar(1.0, 10.0, profiles=O.GaussPortrait(0.5, 0.05, 1.0))
+        tobs, tel, system = 2.0, O.GBT(), "820_GUPPI"
+    else:
+        sig = O.Signal(1500, 800.0, nchan=nchan, samprate=(1.0 / 0.010) * 2048 * 10 ** -6, sublen=60.0, fold=True)
+        psr = O.Pulsar(0.010, 0.005, profiles=O.GaussPortrait(0.5, 0.05, 1.0), specidx=-1.6, ref_freq=1400.0)
+        tobs, tel, system = 60.0 * 20, O.GBT(), "Lband_GUPPI"
+    t0 = time.perf_counter()
+    O.make_pulses(sig, psr, tobs, d)
+    t1 = time.perf_counter()
+    O.disperse(sig, 40.0)
+    t2 = time.perf_counter()
+    O.observe(sig, psr, tel, system, d, noise=True)
+    t3 = time.perf_counter()
+    n = np.asarray(sig.data).shape[1]
+    return {"disperse": nchan * n / (t2 - t1), "disperse_s": t2 - t1, "pipeline": nchan * n / (t3 - t0),
+            "pipeline_s": t3 - t0, "nsamp": n}
+
+
 WORKLOADS = {
     "c2": "C2: NANOGrav L-band search mode 512 ch x 2^20 samp, J1713+0747 DataProfile (P=1/218.81 Hz), "
           "disperse(DM=15.917131) + GBT Lband_GUPPI radiometer noise",
@@ -199,6 +300,10 @@ WORKLOADS = {
           "Arecibo noise",
     "s5": "5-smooth length: 256 ch x 3 125 000 samp (= 2^3 5^8, the reference simulate fixture's sample count), "
           "GaussProfile P=5 ms, disperse(DM=100) + Arecibo noise (radix-5 four-step 1250 x 2500)",
+    "t1": "tutorial_1 (the reference's published search-mode shape): 128 ch x 97 656 samp (2 s at 48.8 kHz, "
+          "2^3 3 13 313: Bluestein), GaussProfile, P=1 s, disperse(DM=40) + GBT 820_GUPPI noise",
+    "t2": "tutorial_2 (the reference's published fold-mode shape): 64 ch x 40 960 samp (20 subints x 2048 bins, "
+          "10 x 4096 mixed radix), P=10 ms, specidx -1.6, disperse(DM=40) + GBT Lband_GUPPI noise",
 }
 
 
@@ -435,6 +540,10 @@ def main():
             args.nchan = 256
         args.log2n = None
         args.no_cpu = True
+    if args.workload in ("t1", "t2"):
+        if args.nchan == NCHAN:
+            args.nchan = 128 if args.workload == "t1" else 64
+        args.log2n = None
     if args.scaling is None:
         args.scaling = "weak" if args.workload == "c5" else "strong"
 
@@ -485,7 +594,7 @@ def main():
             dist.barrier()
         sync()
 
-    nsamp = 30720 if args.workload == "c4" else (S5_NSAMP if args.workload == "s5" else (1 << args.log2n))
+    nsamp = {"c4": 30720, "s5": S5_NSAMP, "t1": T1_NSAMP, "t2": T2_NSAMP}.get(args.workload) or (1 << args.log2n)
 
     def step():
         # the API prints the reference's user warnings (e.g. C4's "sample
@@ -516,6 +625,8 @@ def main():
             return c2_step(pss, total, shard, args.log2n, plan_group=pg)
         if args.workload == "s5":
             return s5_step(pss, total, shard, plan_group=pg)
+        if args.workload in ("t1", "t2"):
+            return tutorial_step(pss, args.workload, total, shard, plan_group=pg)
         return c3_step(pss, total, shard, args.log2n, plan_group=pg)
 
     for _ in range(args.warmup):
@@ -635,6 +746,23 @@ def main():
                          "reference call structure; like the reference it also builds observe's pre-noise "
                          "out copy, ~2%% of its time, which the GPU run elides when ret_resampsig=False), "
                          "single process, %.1f s on %s" % (args.cpu_chans, args.log2n, dt, cpu_model())}
+    tut = None
+    if rank == 0 and world == 1 and not args.dry_run and args.workload in ("t1", "t2"):
+        # the published stage (disperse alone) next to the reference's own
+        # number and the oracle's on this host, same shape
+        pub = PUBLISHED[args.workload]
+        gv, gdt = tutorial_disperse_only(pss, args.workload, total, max(args.steps, 5))
+        tut = {"published_disperse": dict(pub, unit="channel-samples/s", hardware="unstated (the tutorial's "
+                                          "run; BASELINE.md section 1)"),
+               "gpu_disperse_only": {"value": round(gv, 1), "ms": round(gdt * 1e3, 4),
+                                     "vs_published": round(gv / pub["value"], 1)}}
+        if not args.no_cpu:
+            c = cpu_tutorial(args.workload, total)
+            tut["cpu_oracle"] = {"disperse_only": round(c["disperse"], 1), "disperse_s": round(c["disperse_s"], 3),
+                                 "pipeline": round(c["pipeline"], 1), "pipeline_s": round(c["pipeline_s"], 3),
+                                 "cores": 1, "cpu_count": os.cpu_count(), "kind": "port",
+                                 "host": cpu_model()}
+            tut["gpu_disperse_only"]["vs_cpu_oracle"] = round(gv / c["disperse"], 1)
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "channel-samples/s",
@@ -655,6 +783,8 @@ def main():
             "cpu_baseline_allcore": cpu_all,
             "speedup_vs_cpu_allcore": round(value / cpu_all["value"], 1) if cpu_all else None,
         }
+        if tut is not None:
+            line["published_shape"] = tut
         if args.dry_run:
             line["dry_run"] = "host planning only (CPU, gloo): launcher / JSON contract check, not a measurement"
         print(json.dumps(line))

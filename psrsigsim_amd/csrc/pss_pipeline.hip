@@ -74,10 +74,13 @@ static int g_tk_pending = -1;
 
 static int64_t g_tk_units = 0;   // samples processed by the launch being timed
 
+// (the events are created once per slot and reused: creating two events per
+// launch inside the timed steps cost the host ~tens of microseconds each)
 static void tk_begin(int kind, hipStream_t st) {
     if (!g_timing || g_ntl >= 4096) { g_tk_pending = -1; return; }
     TimedLaunch &t = g_tl[g_ntl];
-    if (hipEventCreate(&t.a) != hipSuccess || hipEventCreate(&t.b) != hipSuccess) { g_tk_pending = -1; return; }
+    if (!t.a && hipEventCreate(&t.a) != hipSuccess) { t.a = nullptr; g_tk_pending = -1; return; }
+    if (!t.b && hipEventCreate(&t.b) != hipSuccess) { t.b = nullptr; g_tk_pending = -1; return; }
     t.kind = kind;
     t.units = g_tk_units;
     (void)hipEventRecord(t.a, st);
@@ -3910,8 +3913,6 @@ int pss_timing_collect(int32_t *kind, double *ms, int64_t *units, int cap) {
         (void)hipEventSynchronize(t.b);
         (void)hipEventElapsedTime(&e, t.a, t.b);
         if (n < cap) { kind[n] = t.kind; ms[n] = e; units[n] = t.units; ++n; }
-        (void)hipEventDestroy(t.a);
-        (void)hipEventDestroy(t.b);
     }
     g_ntl = 0;
     return n;

@@ -10,4 +10,5 @@ timeout -k 10 200 python bench.py --workload c4 > $OUT/bench_c4.json 2> $OUT/ben
 timeout -k 10 200 python bench.py --nchan 256 --no-cpu > $OUT/bench_n256.json 2> $OUT/bench_n256.err || exit $?
 timeout -k 10 300 python bench.py --workload c5 --no-cpu > $OUT/bench_c5.json 2> $OUT/bench_c5.err || exit $?
 timeout -k 10 200 python bench.py --workload s5 > $OUT/bench_s5.json 2> $OUT/bench_s5.err || exit $?
-timeout -k 10 300 python tools/k3_bench.py 512 20 1 8 7.3 > $OUT/k3_bench.txt 2>&1 || exit $?
+timeout -k 10 200 python bench.py --workload t1 > $OUT/bench_t1.json 2> $OUT/bench_t1.err || exit $?
+timeout -k 10 200 python bench.py --workload t2 > $OUT/bench_t2.json 2> $OUT/bench_t2.err || exit $?
