@@ -632,30 +632,33 @@ def main():
     for _ in range(args.warmup):
         s = step()
         del s
-    barrier()
+    # stream-ordered step boundaries (the engine launches on the current
+    # stream): the first step's span includes its host planning on an idle
+    # GPU, the later ones are the steady state.  These events and the
+    # library's per-launch timing events are created (first record) before
+    # the barrier, so the timed steps pay no event creation.
+    evs = []
     if not args.dry_run:
         _lib.load().pss_timing_enable(1)
         _lib.timing_collect()
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        for e in evs:
+            e.record()
     power = None if args.dry_run else PowerSampler(torch.cuda.current_device())
+    barrier()
     if power is not None:
         power.start()
     t0 = time.perf_counter()
-    # stream-ordered step boundaries (the engine launches on the current
-    # stream): the first step's span includes its host planning on an idle
-    # GPU, the later ones are the steady state
-    evs = []
-    if not args.dry_run:
-        evs.append(torch.cuda.Event(enable_timing=True))
-        evs[-1].record()
+    if evs:
+        evs[0].record()
     marks = []
-    for _ in range(args.steps):
+    for i in range(args.steps):
         s = step()
         if args.workload == "c4":
             _ = s.data          # fold-mode output is small: materialise it (the gather did when N > 1)
         del s
         if evs:
-            evs.append(torch.cuda.Event(enable_timing=True))
-            evs[-1].record()
+            evs[i + 1].record()
         marks.append(time.perf_counter())
     sync()
     t1 = time.perf_counter()

@@ -2763,8 +2763,12 @@ struct BsArgs {
     const cf *chirp;   // [N]  w_n
     const cf *bhat;    // [M]  permuted order, scaled 1/M
     int64_t N, M, M1, M2;
-    int r0;            // first channel of this batch
-    int mode;          // 0 forward DFT (+ delay ramp), 1 inverse DFT (/N), 2 Bhat build
+    int64_t ld;        // row pitch of src / dst (complex): N, or N rounded up to a 128-B line
+                       // for the fused pair runs' internal rows (rows of N = 2^20 - 2 would
+                       // otherwise start 16 B off a line and split every segment in two)
+    int r0;            // first channel (pair runs: pair) of this batch
+    int mode;          // 0 forward DFT (+ delay ramp), 1 inverse DFT (/N), 2 Bhat build; pair runs:
+                       // 3 inverse DFT's first pass (conj input), 4 forward DFT's last pass (X out)
 };
 
 // w_n = exp(-pi i n^2 / N): n^2 reduced mod 2N exactly, angle in double
@@ -2817,43 +2821,151 @@ __global__ __launch_bounds__(256) void k_bs_col(KP k, BsArgs a) {
     constexpr int B = 8192 / L, T = 256;
     __shared__ cf lds[B * Lds<L>::RS];
     const int tid = threadIdx.x, rb = blockIdx.y, r = a.r0 + rb;
-    const int64_t n20 = (int64_t)blockIdx.x * B;
+    // XCD-aware block order: workgroup ids go round-robin over the 8 XCDs, so
+    // blocks x, x + 8, ... (one XCD) take adjacent column ranges -- a 128-B
+    // line a row offset splits between two neighbouring blocks (rows of N =
+    // 2^20 - 2 complex start 16 B off a line) is fetched once into that
+    // XCD's L2 instead of once per XCD
+    const unsigned gx = gridDim.x;
+    const unsigned bx = (gx & 7) ? blockIdx.x : (blockIdx.x & 7) * (gx >> 3) + (blockIdx.x >> 3);
+    const int64_t n20 = (int64_t)bx * B;
     const float invM = 1.0f / (float)a.M;
     cf *Z = a.Z + (int64_t)rb * a.M;
+    // NI items per thread; the first NH of them hold the rows n1 < M1 / 2,
+    // i.e. n < M / 2: every sample n < N (M >= 2N) lies there, so the later
+    // items are the zero padding (input) / discarded (output) at compile time
+    constexpr int NI = L * B / T, NH = NI / 2;
     // loops unrolled (trip counts are compile-time): every load of a thread
     // in flight together (two 256-thread workgroups per CU leave few waves
     // to hide HBM latency otherwise)
+    if constexpr (KIND == 3) {
+        // pair runs, first pass with the source fused in: both channels of
+        // pair r generated for 4 consecutive samples (one Philox block) per
+        // item, (x_a + i x_b) w_n into the block (k_fb_source_pair's values)
+        static_assert(B >= 4, "fused source: 4-sample items");
+        const int ra = 2 * r - k.poff, rc = ra + 1;
+        const bool hasa = ra >= 0, hasb = rc < k.p.nchan;
+        if (k.p.src == PSS_SRC_LOAD && k.p.null_mode != PSS_NULL_UNDELAYED && hasa && hasb) {
+            // rows already on the device (shift_t, filter_rows, disperse of a
+            // made signal): every load issued before the first is used, as
+            // in the generic first pass; indices clamped, values zeroed
+            // arithmetically past N
+            constexpr int NJ = NH / 4;
+            const float *rowa = k.p.data + (int64_t)ra * k.p.ld, *rowb = rowa + k.p.ld;
+            float xa[NJ][4], xb[NJ][4];
+            cf wv[NJ][4];
 #pragma unroll
-    for (int it = 0; it < L * B / T; ++it) {
-        const int idx = tid + it * T;
-        const int b = idx & (B - 1), n1 = idx / B;
-        const int64_t n = (int64_t)n1 * a.M2 + n20 + b;
-        cf v;
-        if (KIND == 0) {
-            if (a.mode == 2) {
-                const int64_t m = n < a.N ? n : (n > a.M - a.N ? a.M - n : -1);
-                v = m >= 0 ? make_float2(a.chirp[m].x, -a.chirp[m].y) : make_float2(0.f, 0.f);
-            } else if (n < a.N) {
-                v = cmul(a.src[(int64_t)r * a.N + n], a.chirp[n]);
-            } else {
-                v = make_float2(0.f, 0.f);
+            for (int it = 0; it < NJ; ++it) {
+                const int idx = tid + it * T;
+                const int64_t n = (int64_t)(idx / (B / 4)) * a.M2 + n20 + (idx % (B / 4)) * 4;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int64_t nc = n + i < a.N ? n + i : 0;
+                    xa[it][i] = rowa[nc];
+                    xb[it][i] = rowb[nc];
+                    wv[it][i] = a.chirp[nc];
+                }
             }
-        } else {
-            // Q[k1 = n1][n2] * exp(+2 pi i n2 k1 / M)
-            v = cmul(Z[n], bs_twiddle((n20 + b) * n1, a.M, invM, true));
+#pragma unroll
+            for (int it = 0; it < NI / 4; ++it) {
+                const int idx = tid + it * T;
+                const int b4 = (idx % (B / 4)) * 4, n1 = idx / (B / 4);
+                const int64_t n = (int64_t)n1 * a.M2 + n20 + b4;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    cf v = make_float2(0.f, 0.f);
+                    if (it < NJ) {
+                        const float f = n + i < a.N ? 1.0f : 0.0f;
+                        v = cmul(make_float2(xa[it][i], xb[it][i]), wv[it][i]);
+                        v = make_float2(v.x * f, v.y * f);
+                    }
+                    lds[Lds<L>::at(b4 + i, n1)] = v;
+                }
+            }
+        } else
+#pragma unroll
+        for (int it = 0; it < NI / 4; ++it) {
+            const int idx = tid + it * T;
+            const int b4 = (idx % (B / 4)) * 4, n1 = idx / (B / 4);
+            const int64_t n = (int64_t)n1 * a.M2 + n20 + b4;
+            float xa[4] = {0.f, 0.f, 0.f, 0.f}, xb[4] = {0.f, 0.f, 0.f, 0.f}, dum[4];
+            const int cnt = (it < NH / 4 && n < a.N) ? (int)min((int64_t)4, a.N - n) : 0;
+            if (cnt) {
+                if (hasa) source4(k, ra, n, cnt, xa, dum, true, false);
+                if (hasb) source4(k, rc, n, cnt, xb, dum, true, false);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                lds[Lds<L>::at(b4 + i, n1)] = i < cnt ? cmul(make_float2(xa[i], xb[i]), a.chirp[n + i])
+                                                     : make_float2(0.f, 0.f);
         }
-        lds[Lds<L>::at(b, n1)] = v;
-    }
-    __syncthreads();
-    BsFft<L, B, T, R>::template go<KIND != 0>(lds, tid);
-    if (KIND == 2) {
+    } else if (KIND == 0 && a.mode == 2) {
+        // the Bhat build (one row, once per run): b_m = conj(w_m) for m < N,
+        // conj(w_{M-m}) for m > M - N
 #pragma unroll
         for (int it = 0; it < L * B / T; ++it) {
             const int idx = tid + it * T;
             const int b = idx & (B - 1), n1 = idx / B;
+            const int64_t n = (int64_t)n1 * a.M2 + n20 + b;
+            const int64_t m = n < a.N ? n : (n > a.M - a.N ? a.M - n : -1);
+            lds[Lds<L>::at(b, n1)] = m >= 0 ? make_float2(a.chirp[m].x, -a.chirp[m].y) : make_float2(0.f, 0.f);
+        }
+    } else {
+        // Every load of the block issued before the first value is used (two
+        // 256-thread workgroups per CU: few waves to hide HBM latency).  As
+        // one loop the compiler interleaved loads and LDS stores, 4 loads in
+        // flight per wave; and a select around the first pass's loads became
+        // a branch per item, each waiting on its own loads.
+        constexpr int NL = KIND == 0 ? NH : NI;     // items loaded
+        cf va[NL], vb[KIND == 0 ? NL : 1];
+#pragma unroll
+        for (int it = 0; it < NL; ++it) {
+            const int idx = tid + it * T;
+            const int b = idx & (B - 1), n1 = idx / B;
+            const int64_t n = (int64_t)n1 * a.M2 + n20 + b;
+            if (KIND == 0) {
+                // a_n = x_n w_n (mode 3, pair runs' inverse DFT: conj(Y_n) w_n);
+                // index clamped, the value zeroed arithmetically below
+                const int64_t nc = n < a.N ? n : 0;
+                va[it] = a.src[(int64_t)r * a.ld + nc];
+                vb[it] = a.chirp[nc];
+            } else {
+                va[it] = Z[n];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < NI; ++it) {
+            const int idx = tid + it * T;
+            const int b = idx & (B - 1), n1 = idx / B;
+            const int64_t n = (int64_t)n1 * a.M2 + n20 + b;
+            cf v;
+            if (KIND == 0) {
+                if (it < NL) {
+                    const float f = n < a.N ? 1.0f : 0.0f;
+                    v = cmul(a.mode == 3 ? make_float2(va[it].x, -va[it].y) : va[it], vb[it]);
+                    v = make_float2(v.x * f, v.y * f);
+                } else {
+                    v = make_float2(0.f, 0.f);
+                }
+            } else {
+                // Q[k1 = n1][n2] * exp(+2 pi i n2 k1 / M)
+                v = cmul(va[it], bs_twiddle((n20 + b) * n1, a.M, invM, true));
+            }
+            lds[Lds<L>::at(b, n1)] = v;
+        }
+    }
+    __syncthreads();
+    BsFft<L, B, T, R>::template go<KIND != 0 && KIND != 3>(lds, tid);
+    if (KIND == 2) {
+        int mtid = tid;                 // (opaque: see the output loop's otid)
+        asm volatile("" : "+v"(mtid));
+#pragma unroll
+        for (int it = 0; it < L * B / T; ++it) {
+            const int idx = mtid + it * T;
+            const int b = idx & (B - 1), n1 = idx / B;
             const int64_t pos = (int64_t)n1 * a.M2 + n20 + b;
             cf v = make_float2(0.f, 0.f);
-            if (pos < a.N) {
+            if (it < NH && pos < a.N) {
                 const cf w = a.chirp[pos];
                 const cf X = apply_ramp(k, r, pos, cmul(lds[Lds<L>::at(b, n1)], w));
                 v = cmul(make_float2(X.x, -X.y), w);
@@ -2864,18 +2976,156 @@ __global__ __launch_bounds__(256) void k_bs_col(KP k, BsArgs a) {
         BsFft<L, B, T, R>::template go<false>(lds, tid);
     }
     const float invN = 1.0f / (float)a.N;
+    // the output loop's indices and twiddles from an opaque copy of the
+    // thread id: computed here, not hoisted above the FFT and held through it
+    // (that had KIND 0 at 294 VGPRs, one wave per SIMD)
+    int otid = tid;
+    asm volatile("" : "+v"(otid));
+    // KIND 1 / 4: the chirp at this thread's output positions, all loaded
+    // before the first is used (as a load inside the output loop each item's
+    // store waited on its own load; loaded with the input instead, the
+    // values held through the FFT pushed the kernel past 256 VGPRs)
+    cf cw[(KIND == 1 || KIND == 4) ? NH : 1];
+    if constexpr (KIND == 1 || KIND == 4) {
 #pragma unroll
-    for (int it = 0; it < L * B / T; ++it) {
-        const int idx = tid + it * T;
+        for (int it = 0; it < NH; ++it) {
+            int64_t pos;
+            if constexpr (KIND == 1) {          // the output loop's items
+                const int idx = otid + it * T;
+                pos = (int64_t)(idx / B) * a.M2 + n20 + (idx & (B - 1));
+            } else {                            // 4-sample items: it = 4 item + i
+                const int idx = otid + (it >> 2) * T;
+                pos = (int64_t)(idx / (B / 4)) * a.M2 + n20 + (idx % (B / 4)) * 4 + (it & 3);
+            }
+            cw[it] = a.chirp[pos < a.N ? pos : 0];
+        }
+    }
+    if constexpr (KIND == 4) {
+        // pair runs, last pass with the epilogue fused in: y = conj(conv_n
+        // w_n) / N = (y_a + i y_b) of 4 consecutive samples per item, each
+        // channel's epilogue (null replacement, observe copy, noise, store)
+        // straight from the block (k_fb_epilogue_pair's values)
+        static_assert(B >= 4, "fused epilogue: 4-sample items");
+        const int ra = 2 * r - k.poff, rc = ra + 1;
+        const bool hasa = ra >= 0, hasb = rc < k.p.nchan;
+        const float msk[4] = {0.f, 0.f, 0.f, 0.f};
+        // y = conj(conv w) / N back into the thread's own LDS entries first
+        // (a small loop, unrolled: cw stays in registers; the epilogue loop
+        // below is too large to unroll, and indexing cw there put it in scratch)
+#pragma unroll
+        for (int it = 0; it < NH / 4; ++it) {
+            const int idx = otid + it * T;
+            const int b4 = (idx % (B / 4)) * 4, k1 = idx / (B / 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const cf v = cmul(lds[Lds<L>::at(b4 + i, k1)], cw[4 * it + i]);
+                lds[Lds<L>::at(b4 + i, k1)] = make_float2(v.x * invN, -v.y * invN);
+            }
+        }
+        for (int it = 0; it < NH / 4; ++it) {
+            const int idx = otid + it * T;
+            const int b4 = (idx % (B / 4)) * 4, k1 = idx / (B / 4);
+            const int64_t pos = (int64_t)k1 * a.M2 + n20 + b4;
+            if (pos >= a.N) continue;
+            const int cnt = (int)min((int64_t)4, a.N - pos);
+            float ya[4] = {0.f, 0.f, 0.f, 0.f}, yb[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (i < cnt) {
+                    const cf v = lds[Lds<L>::at(b4 + i, k1)];
+                    ya[i] = v.x;
+                    yb[i] = v.y;
+                }
+            }
+            if (hasa) epilogue4(k, ra, pos, cnt, ya, msk, false);
+            if (hasb) epilogue4(k, rc, pos, cnt, yb, msk, false);
+        }
+        return;
+    }
+#pragma unroll
+    for (int it = 0; it < (KIND == 1 ? NH : NI); ++it) {
+        const int idx = otid + it * T;
         const int b = idx & (B - 1), k1 = idx / B;
         const int64_t n2 = n20 + b, pos = (int64_t)k1 * a.M2 + n2;
         cf v = lds[Lds<L>::at(b, k1)];
         if (KIND != 1) {
             Z[pos] = cmul(v, bs_twiddle(n2 * k1, a.M, invM, false));
         } else if (pos < a.N) {                 // pos = n1 M2 + n2: output sample
-            v = cmul(v, a.chirp[pos]);
-            a.dst[(int64_t)r * a.N + pos] = make_float2(v.x * invN, -v.y * invN);
+            v = cmul(v, cw[KIND == 1 ? it : 0]);
+            // mode 4 (pair runs: the forward DFT's last pass): X_n, unscaled
+            a.dst[(int64_t)r * a.ld + pos] = a.mode == 4 ? v : make_float2(v.x * invN, -v.y * invN);
         }
+    }
+}
+
+// Pair runs (no delayed null: two real channels per complex Bluestein row,
+// half the transforms).  Between the forward DFT (X, natural order, in W1)
+// and the inverse: per pair row and bin k <= N/2, the two channels'
+// spectra A = (X_k + conj X_{N-k}) / 2, B = (X_k - conj X_{N-k}) / 2i, each
+// times its own channel's ramp / transfer function (apply_ramp: A and B are
+// real at DC and Nyquist, so the real-part rule applies), recombined as
+// Y_k = A' + i B', Y_{N-k} = conj A' + i conj B'.  In place; rows of the
+// batch starting at pair r0 (local channel rows 2 p - poff, 2 p + 1 - poff).
+__global__ __launch_bounds__(256) void k_bs_sep(KP k, cf *X, int64_t ld, int r0) {
+    const int p = r0 + (int)blockIdx.y;
+    const int ra = 2 * p - k.poff, rb = ra + 1;
+    const int ca = max(ra, 0), cb = min(rb, k.p.nchan - 1);
+    const int64_t N = k.N, H = N / 2;
+    cf *x = X + (int64_t)p * ld;
+    for (int64_t kb = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; kb <= H;
+         kb += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t km = kb ? N - kb : 0;
+        const cf z = x[kb], zm = x[km];
+        cf A = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+        cf B = make_float2(0.5f * (z.y + zm.y), 0.5f * (zm.x - z.x));
+        if (kb == 0 || kb == H) {                     // real bins (rounding residue dropped)
+            A.y = 0.0f;
+            B.y = 0.0f;
+        }
+        A = apply_ramp(k, ca, kb, A);
+        B = apply_ramp(k, cb, kb, B);
+        x[kb] = make_float2(A.x - B.y, A.y + B.x);
+        if (kb != km) x[km] = make_float2(A.x + B.y, B.x - A.y);
+    }
+}
+
+// Pair runs: source of both channels of a pair into one complex row, and the
+// epilogue of both from it (the k_fb_source / k_fb_epilogue of the channel rows).
+__global__ __launch_bounds__(256) void k_fb_source_pair(KP k) {
+    const int p = blockIdx.y;
+    const int ra = 2 * p - k.poff, rb = ra + 1;
+    const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
+    cf *W1 = reinterpret_cast<cf *>(k.p.work) + (int64_t)p * k.N;
+    const int64_t items = (k.N + 3) >> 2;
+    for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < items;
+         it += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t n0 = it << 2;
+        const int cnt = (int)min((int64_t)4, k.N - n0);
+        float a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0}, dum[4];
+        if (hasa) source4(k, ra, n0, cnt, a, dum, true, false);
+        if (hasb) source4(k, rb, n0, cnt, b, dum, true, false);
+        for (int i = 0; i < cnt; ++i) W1[n0 + i] = make_float2(a[i], b[i]);
+    }
+}
+__global__ __launch_bounds__(256) void k_fb_epilogue_pair(KP k) {
+    const int p = blockIdx.y;
+    const int ra = 2 * p - k.poff, rb = ra + 1;
+    const bool hasa = ra >= 0, hasb = rb < k.p.nchan;
+    const cf *W1 = reinterpret_cast<const cf *>(k.p.work) + (int64_t)p * k.N;
+    const int64_t items = (k.N + 3) >> 2;
+    for (int64_t it = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; it < items;
+         it += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t n0 = it << 2;
+        const int cnt = (int)min((int64_t)4, k.N - n0);
+        float a[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+        const float msk[4] = {0, 0, 0, 0};
+        for (int i = 0; i < cnt; ++i) {
+            const cf z = W1[n0 + i];
+            a[i] = z.x;
+            b[i] = z.y;
+        }
+        if (hasa) epilogue4(k, ra, n0, cnt, a, msk, false);
+        if (hasb) epilogue4(k, rb, n0, cnt, b, msk, false);
     }
 }
 
@@ -3180,7 +3430,7 @@ static BsGeom bs_geom(int32_t nchan, int64_t N) {
     while (g.M < 2 * N - 1) g.M <<= 1;
     g.M2 = g.M >= (1ll << 25) ? 8192 : 4096;
     g.M1 = g.M / g.M2;
-    g.nb = ((int64_t)nchan * N) / g.M;
+    g.nb = ((int64_t)nchan * N + g.M - 1) / g.M;    // (ceil: no near-empty last batch)
     if (g.nb < 1) g.nb = 1;
     if (g.nb > nchan) g.nb = nchan;
     if (g.nb > 65535) g.nb = 65535;
@@ -3494,7 +3744,9 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
         // (PairRowsSeq); no transfer function / tail variant (run_fourstep
         // keeps those runs on the 2048 x 8192 split)
         if (k.p.htab || k.p.tail_a) return fail(PSS_EUNSUPPORTED, "%d-point rows: no transfer function", N2);
-        constexpr int TS = N2 / 16;                  // 16 values of each row per thread
+        // (16 values of each row per thread: 512 threads with 32 measured
+        // 47.8 against 43.9 ms at C5, profiles/r05/r16/)
+        constexpr int TS = N2 / 16;
         using PRS = PairRowsSeq<N2, TS, RF, RI>;
         k_pair_row_seq<PRS, TS, false><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2 - 1)), dim3(TS), 0, st>>>(k);
         k_pair_row_seq<PRS, TS, true><<<dim3((unsigned)k.npairs, 1u), dim3(TS), 0, st>>>(k);
@@ -3677,7 +3929,13 @@ static int bs_col(const KP &k, const BsArgs &a, int rows, int kind, hipStream_t 
     dim3 g((unsigned)(a.M2 / (8192 / L)), (unsigned)rows);
     if (kind == 0) k_bs_col<L, R, 0><<<g, dim3(256), 0, st>>>(k, a);
     else if (kind == 1) k_bs_col<L, R, 1><<<g, dim3(256), 0, st>>>(k, a);
-    else k_bs_col<L, R, 2><<<g, dim3(256), 0, st>>>(k, a);
+    else if (kind == 2) k_bs_col<L, R, 2><<<g, dim3(256), 0, st>>>(k, a);
+    else if constexpr (L <= 2048) {
+        if (kind == 3) k_bs_col<L, R, 3><<<g, dim3(256), 0, st>>>(k, a);
+        else k_bs_col<L, R, 4><<<g, dim3(256), 0, st>>>(k, a);
+    } else {
+        return fail(PSS_EUNSUPPORTED, "Bluestein: fused pair passes need M1 <= 2048");
+    }
     LAUNCHCHK();
     return PSS_OK;
 }
@@ -3730,6 +3988,39 @@ static int bs_filter(const KP &k, BsArgs a, int64_t nb, hipStream_t st) {
     return PSS_OK;
 }
 
+// Pair runs: forward DFT (X in src, natural order) -> channel separation,
+// ramps, recombination (k_bs_sep) -> inverse DFT / N, per batch of nb pair
+// rows: 6 passes over M and one over N instead of 5 over M for each of the
+// two channels.
+static bool bs_fused(const BsArgs &a) { return a.M1 <= 2048; }   // 8192 / M1 >= 4 columns per block
+
+static int bs_filter_pair(const KP &k, BsArgs a, int64_t nb, int npairs, hipStream_t st) {
+    const bool fused = bs_fused(a);
+    for (int64_t r0 = 0; r0 < npairs; r0 += nb) {
+        const int rows = (int)((npairs - r0) < nb ? (npairs - r0) : nb);
+        a.r0 = (int)r0;
+        BsArgs f = a, g = a;
+        f.mode = 4;                 // forward: ..., X -> src (consumed by its first pass)
+        f.dst = const_cast<cf *>(a.src);
+        g.mode = 3;                 // inverse: conj(Y) w -> ..., result -> dst
+        // (fused: the first pass generates the source, the last runs the epilogue)
+        int rc = bs_col_any(k, a, rows, fused ? 3 : 0, st);
+        if (!rc) rc = bs_row_any(k, a, rows, st);
+        if (!rc) rc = bs_col_any(k, f, rows, 1, st);
+        if (!rc) {
+            k_bs_sep<<<dim3((unsigned)std::min<int64_t>((k.N / 2 + 256) / 256, 1024), (unsigned)rows), dim3(256), 0,
+                       st>>>(k, const_cast<cf *>(a.src), a.ld, (int)r0);
+            HIPCHK(hipGetLastError());
+        }
+        if (!rc) rc = bs_col_any(k, g, rows, 0, st);
+        if (!rc) rc = bs_row_any(k, g, rows, st);
+        g.mode = 1;
+        if (!rc) rc = bs_col_any(k, g, rows, fused ? 4 : 1, st);
+        if (rc) return rc;
+    }
+    return PSS_OK;
+}
+
 // The float64 null decisions of the packed paths (k_null_refine), between
 // the inverse transform (W1 = data + i mask per row) and the epilogue.
 static bool refine_null(const KP &k) {
@@ -3774,12 +4065,24 @@ static int run_bluestein(KP &k, hipStream_t st) {
     a.chirp = reinterpret_cast<const cf *>(base + w.bs_chirp);
     a.bhat = reinterpret_cast<const cf *>(base + w.bs_bhat);
     a.N = k.N;
+    a.ld = k.N;
     a.M = g.M;
     a.M1 = g.M1;
     a.M2 = g.M2;
-    dim3 ge = stream_grid((k.N + 3) / 4, k.p.nchan);
+    // two channels per complex row unless a delayed null rides in the
+    // imaginary part (its mask shares the channel's transform)
+    const bool pair = k.p.null_mode != PSS_NULL_DELAYED;
+    k.poff = k.p.chan0 & 1;                 // pairs of (even, odd) GLOBAL channels: shard invariant
+    k.npairs = (k.p.nchan + k.poff + 1) / 2;
+    dim3 ge = stream_grid((k.N + 3) / 4, pair ? k.npairs : k.p.nchan);
+    const bool fused = pair && g.M1 <= 2048;      // (bs_fused)
+    // fused pair runs: W1's rows are internal (no source / epilogue kernel
+    // reads them), so they may start on 128-B lines where W1 has the room
+    const int64_t ldp = (k.N + 15) & ~(int64_t)15;
+    if (fused && k.npairs * ldp <= (int64_t)k.p.nchan * k.N) a.ld = ldp;
     tk_begin(TK_FALLBACK, st);
-    k_fb_source<<<ge, dim3(256), 0, st>>>(k);
+    if (!pair) k_fb_source<<<ge, dim3(256), 0, st>>>(k);
+    else if (!fused) k_fb_source_pair<<<ge, dim3(256), 0, st>>>(k);
     LAUNCHCHK();
     k_bs_chirp<<<stream_grid(k.N, 1), dim3(256), 0, st>>>(reinterpret_cast<cf *>(base + w.bs_chirp), k.N);
     LAUNCHCHK();
@@ -3793,6 +4096,13 @@ static int run_bluestein(KP &k, hipStream_t st) {
     a.src = W1;
     a.dst = W1;
     a.mode = 0;
+    if (pair) {
+        if ((rc = bs_filter_pair(k, a, g.nb, k.npairs, st))) return rc;
+        if (!fused) k_fb_epilogue_pair<<<ge, dim3(256), 0, st>>>(k);
+        tk_end(st);
+        LAUNCHCHK();
+        return PSS_OK;
+    }
     if ((rc = bs_filter(k, a, g.nb, st))) return rc;
     if (refine_null(k) && (rc = launch_null_refine(k, st))) return rc;
     k_fb_epilogue<<<ge, dim3(256), 0, st>>>(k);
@@ -3895,6 +4205,11 @@ int pss_set_flags(int flags) {
 
 void pss_timing_enable(int on) {
     g_timing = on != 0;
+    // create the first slots' events now, not inside the first timed run
+    for (int i = 0; g_timing && i < 512; ++i) {
+        if (!g_tl[i].a && hipEventCreate(&g_tl[i].a) != hipSuccess) g_tl[i].a = nullptr;
+        if (!g_tl[i].b && hipEventCreate(&g_tl[i].b) != hipSuccess) g_tl[i].b = nullptr;
+    }
 }
 
 double pss_timing_span_ms(void) {
