@@ -722,7 +722,27 @@ def main():
                                        "/ ms_per_step / (8 TB/s x n_gpus)"}
         # measured HBM bytes per launch of this kernel (rocprofv3 PMC passes,
         # tools/pmc_round.sh + tools/pmc_traffic.py; C3 size only)
-        for rnd in ("r04", "r03", "r02"):
+        # the rocprofv3 kernel trace of the same C3 run (tools/prof_summary.py
+        # --json, full-size launches): which kernel dominates there and its
+        # fraction, reported next to this run's HIP-event figures (the two
+        # rankings can differ box to box)
+        for rnd in ("r05", "r04"):
+            kj = os.path.join(ROOT, "profiles", rnd, "kernel_profile.json")
+            if args.workload == "c3" and C == NCHAN and nsamp == (1 << LOG2N) and os.path.exists(kj):
+                kp = json.load(open(kj))
+                kp = {k: v for k, v in kp.items() if k in ALG_BYTES}
+                if kp:
+                    pd = max(kp, key=lambda k: kp[k]["avg_ms"])
+                    fr = {k: round(ALG_BYTES[k] * full / (v["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                          for k, v in kp.items()}
+                    roof["frac_profile"] = fr[pd]
+                    roof["kernel_profile"] = pd
+                    roof["avg_launch_ms_profile"] = kp[pd]["avg_ms"]
+                    roof["frac_profile_same_kernel"] = fr.get(dom)
+                    roof["frac_profile_source"] = "profiles/%s/kernel_profile.json (rocprofv3 kernel trace, " \
+                                                  "full-size launches)" % rnd
+                break
+        for rnd in ("r05", "r04", "r03", "r02"):
             tj = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
             if args.workload == "c3" and C == NCHAN and nsamp == (1 << LOG2N) and os.path.exists(tj):
                 t = json.load(open(tj)).get(dom)
