@@ -683,6 +683,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     per_step = elapsed / args.steps
+    n_devices = 1 if args.same_device else world
     units = float(total) * nsamp
     value = units / per_step
 
@@ -717,9 +718,10 @@ def main():
                 "avg_launch_ms": round(avg_ms, 4), "alg_bytes_per_launch": bytes_launch,
                 "pipeline_alg_bytes_per_step": step_bytes,
                 "pipeline_achieved": round(step_bytes / per_step / 1e9, 1),
-                "pipeline_frac": round(step_bytes / per_step / 1e9 / (HBM_PEAK_GBS * world), 4),
+                # (--same-device rehearsals: every rank on one card, one HBM)
+                "pipeline_frac": round(step_bytes / per_step / 1e9 / (HBM_PEAK_GBS * n_devices), 4),
                 "pipeline_frac_basis": "all kernels' algorithmic bytes per step (ALG_BYTES x channel-samples) "
-                                       "/ ms_per_step / (8 TB/s x n_gpus)"}
+                                       "/ ms_per_step / (8 TB/s x n_devices)"}
         # measured HBM bytes per launch of this kernel (rocprofv3 PMC passes,
         # tools/pmc_round.sh + tools/pmc_traffic.py; C3 size only)
         # the rocprofv3 kernel trace of the same C3 run (tools/prof_summary.py
@@ -789,7 +791,7 @@ def main():
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "channel-samples/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "n_gpus": world, "n_devices": n_devices, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(per_step * 1e3, 3), "higher_is_better": True, "scaling": args.scaling,
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (Philox chi2 pulses/noise)",
             "config": {"workload": WORKLOADS[args.workload], "nchan_total": total,
