@@ -2597,12 +2597,30 @@ __global__ __launch_bounds__(256) void k_fb_epilogue(KP k) {
 // s = the channel's ramp (frac(delay/N)), nyq its mask Nyquist factor -- the
 // reference's shift_t of the box row by the total delay (pulsar.py:306-330,
 // utils.py:17-59) -- and its decision m > 1 replaces the fp32 one (encoded as
-// mask 2 / 0 for the epilogue).  One wave per candidate sample, the bins split
-// over the lanes (phasor recurrences from one sincospi per lane), a wave sum.
+// mask 2 / 0 for the epilogue).  The candidates are first compacted into a
+// list (k_null_cands), then one wave per candidate (k_null_refine_list, the
+// waves striding over the list: candidates cluster at the box edges, so a
+// wave per 64 samples left a few waves with most of the work -- C4's
+// geometry with a null: 26.7 ms of refine), the bins split over the lanes in
+// four interleaved phasor recurrences (independent chains: the recurrence's
+// float64 latency no longer serialises the loop), a wave sum.  A list that
+// would overflow its capacity falls back to the per-sample kernel
+// (k_null_refine) for the whole run.  The box spectrum is summed in kBsParts
+// sample ranges (all CUs busy; all-zero 1024-sample tiles skipped), then
+// reduced in a fixed order (run to run the same bits).
 // Even N <= kRefineMaxN (the O(N x nnz) box spectrum), no scattering tail
 // (an extension whose packed path also filters the mask).
 // ---------------------------------------------------------------------------
 static constexpr int64_t kRefineMaxN = 1 << 17;
+static constexpr int kBsParts = 16;
+// refine candidate list capacity (entries of 8 B): 1/8 of the samples + 64 Ki
+// (C4's fold-mode geometry with a null has ~7 % candidates: its boxes are
+// chi2(Nfold ~ 1e4) values, so the band is ~0.3 wide and the boxes' Gibbs
+// ringing crosses it often)
+static inline int64_t refine_cap(int32_t nchan, int64_t N) {
+    const int64_t all = (int64_t)nchan * N;
+    return std::min<int64_t>(all, all / 8 + 65536);
+}
 
 __global__ __launch_bounds__(256) void k_tw64(int64_t N, double2 *tw) {
     for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; n < N; n += (int64_t)gridDim.x * 256) {
@@ -2612,19 +2630,27 @@ __global__ __launch_bounds__(256) void k_tw64(int64_t N, double2 *tw) {
     }
 }
 
-// B_k = sum_n box[n] e^{-2 pi i k n / N}, k <= N/2 (float64; the tile loop is
-// uniform over the workgroup, so skipping zero box samples does not diverge)
-__global__ __launch_bounds__(256) void k_null_bspec(const float *box, int64_t N, const double2 *tw, double2 *B) {
+// partial box spectra: part[p][k] = sum_{n in range p} box[n] e^{-2 pi i k n / N},
+// k <= N/2, float64 (grid: bins / 256 x kBsParts sample ranges; the tile
+// loop is uniform over the workgroup, so skipping zero tiles / samples does
+// not diverge)
+__global__ __launch_bounds__(256) void k_null_bspec(const float *box, int64_t N, const double2 *tw, double2 *part) {
     __shared__ float tile[1024];
     const int64_t K = N / 2 + 1;
     const int64_t kb = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t kk = kb < K ? kb : 0;
+    const int64_t n0 = N * (int64_t)blockIdx.y / kBsParts, n1 = N * ((int64_t)blockIdx.y + 1) / kBsParts;
     double re = 0.0, im = 0.0;
-    for (int64_t base = 0; base < N; base += 1024) {
-        const int cnt = (int)min((int64_t)1024, N - base);
+    for (int64_t base = n0; base < n1; base += 1024) {
+        const int cnt = (int)min((int64_t)1024, n1 - base);
         __syncthreads();
-        for (int i = threadIdx.x; i < cnt; i += 256) tile[i] = box[base + i];
-        __syncthreads();
+        int nz = 0;
+        for (int i = threadIdx.x; i < cnt; i += 256) {
+            const float b = box[base + i];
+            tile[i] = b;
+            nz |= b != 0.0f;
+        }
+        if (!__syncthreads_or(nz)) continue;          // (the barrier also orders the tile)
         int64_t m = (kk * base) % N;
         for (int i = 0; i < cnt; ++i) {
             const float b = tile[i];
@@ -2637,7 +2663,21 @@ __global__ __launch_bounds__(256) void k_null_bspec(const float *box, int64_t N,
             if (m >= N) m -= N;
         }
     }
-    if (kb < K) B[kb] = make_double2(re, im);
+    if (kb < K) part[(int64_t)blockIdx.y * K + kb] = make_double2(re, im);
+}
+
+// B_k = the parts summed in a fixed order
+__global__ __launch_bounds__(256) void k_null_bsum(const double2 *part, int64_t K, double2 *B) {
+    const int64_t kb = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (kb >= K) return;
+    double re = 0.0, im = 0.0;
+#pragma unroll
+    for (int p = 0; p < kBsParts; ++p) {
+        const double2 v = part[(int64_t)p * K + kb];
+        re += v.x;
+        im += v.y;
+    }
+    B[kb] = make_double2(re, im);
 }
 
 // per row: the largest |value| of the packed inverse (data and mask parts),
@@ -2654,43 +2694,133 @@ __global__ __launch_bounds__(256) void k_row_absmax(const cf *W1, int64_t N, uns
     if ((threadIdx.x & 63) == 0) atomicMax(mx + r, __float_as_uint(v));
 }
 
-__global__ __launch_bounds__(256) void k_null_refine(KP k, cf *W1, const double2 *B, const unsigned int *mx) {
+// the float64 mask value m(n) at sample ns of channel r; wave-wide (every lane
+// of the wave calls it for the same (r, ns)), the result valid in every lane
+__device__ __forceinline__ double refine_mask(const KP &k, const double2 *B, int r, int64_t ns, int lane) {
+    const int64_t N = k.N, H = N / 2;
+    const double ramp = (double)k.p.ramp[r] * 5.421010862427522e-20;     // 2^-64
+    // per-bin phase step (revolutions): n/N - s
+    double phi = (double)ns / (double)N - ramp;
+    phi -= floor(phi);
+    // lane's bins k = 1 + lane + 64 j in four chains (j mod 4), each a
+    // phasor recurrence of step e^{2 pi i 256 phi}
+    double sn[4], cs[4], acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        sincospi(2.0 * phi * (double)(1 + lane + 64 * c), &sn[c], &cs[c]);
+        acc[c] = 0.0;
+    }
+    double s256, c256;
+    sincospi(2.0 * phi * 256.0, &s256, &c256);
+    for (int64_t kb = 1 + lane; kb < H; kb += 256) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int64_t kc = kb + 64 * c;
+            const double2 b = B[kc < H ? kc : 0];
+            const double f = kc < H ? 1.0 : 0.0;
+            acc[c] = fma(f * b.x, cs[c], fma(-f * b.y, sn[c], acc[c]));
+            const double t = cs[c] * c256 - sn[c] * s256;
+            sn[c] = cs[c] * s256 + sn[c] * c256;
+            cs[c] = t;
+        }
+    }
+    double a = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+    double m = B[0].x + 2.0 * a;
+    if (2 * H == N) m += B[H].x * (double)k.p.nyq_im[r] * ((ns & 1) ? -1.0 : 1.0);
+    return m / (double)N;
+}
+
+static __device__ __forceinline__ bool refine_cand(const cf *z, int64_t n, int64_t N, float band) {
+    return n < N && fabsf(z[n < N ? n : 0].y - 1.0f) < band;
+}
+
+// candidates of every row into the list (entry = r << 32 | n; order free:
+// each entry's decision is computed on its own)
+__global__ __launch_bounds__(256) void k_null_cands(KP k, const cf *W1, const unsigned int *mx,
+                                                   unsigned long long *list, unsigned int *cnt, int64_t cap) {
+    const int r = blockIdx.y, lane = threadIdx.x & 63;
+    const int64_t N = k.N;
+    const float band = fmaxf(1e-3f, 3e-5f * __uint_as_float(mx[r]));
+    const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool cand = refine_cand(W1 + (int64_t)r * N, n, N, band);
+    const uint64_t m = __ballot(cand);
+    if (!m) return;
+    unsigned int b0 = 0;
+    if (lane == 0) b0 = atomicAdd(cnt, (unsigned int)__popcll(m));
+    b0 = __shfl(b0, 0);
+    if (cand) {
+        const int64_t idx = (int64_t)b0 + __popcll(m & ((1ull << lane) - 1ull));
+        if (idx < cap) list[idx] = ((unsigned long long)r << 32) | (unsigned long long)n;
+    }
+}
+
+// four candidates per wave: every bin's B_k load serves four phasor
+// recurrences (the candidates' independent chains), a quarter of the L2
+// traffic of one candidate per wave
+__global__ __launch_bounds__(256) void k_null_refine_list(KP k, cf *W1, const double2 *B,
+                                                         const unsigned long long *list, const unsigned int *cnt,
+                                                         int64_t cap) {
+    constexpr int C = 4;
+    const int lane = threadIdx.x & 63;
+    const int64_t total = min((int64_t)*cnt, cap);
+    const int64_t N = k.N, H = N / 2;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t e0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * C; e0 < total; e0 += nw * C) {
+        int r[C];
+        int64_t ns[C];
+        double sn[C], cs[C], s64[C], c64[C], acc[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int64_t e = e0 + c < total ? e0 + c : e0;           // (a repeat of e0: not written)
+            const unsigned long long v = list[e];
+            r[c] = (int)(v >> 32);
+            ns[c] = (int64_t)(v & 0xffffffffull);
+            double phi = (double)ns[c] / (double)N - (double)k.p.ramp[r[c]] * 5.421010862427522e-20;
+            phi -= floor(phi);
+            sincospi(2.0 * phi * (double)(1 + lane), &sn[c], &cs[c]);
+            sincospi(2.0 * phi * 64.0, &s64[c], &c64[c]);
+            acc[c] = 0.0;
+        }
+        for (int64_t kb = 1 + lane; kb < H; kb += 64) {
+            const double2 b = B[kb];
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                acc[c] = fma(b.x, cs[c], fma(-b.y, sn[c], acc[c]));
+                const double t = cs[c] * c64[c] - sn[c] * s64[c];
+                sn[c] = cs[c] * s64[c] + sn[c] * c64[c];
+                cs[c] = t;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            double a = acc[c];
+            for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+            double m = B[0].x + 2.0 * a;
+            if (2 * H == N) m += B[H].x * (double)k.p.nyq_im[r[c]] * ((ns[c] & 1) ? -1.0 : 1.0);
+            m /= (double)N;
+            if (lane == 0 && e0 + c < total) W1[(int64_t)r[c] * N + ns[c]].y = m > 1.0 ? 2.0f : 0.0f;
+        }
+    }
+}
+
+// the per-sample form: only when the candidate list overflowed its capacity
+__global__ __launch_bounds__(256) void k_null_refine(KP k, cf *W1, const double2 *B, const unsigned int *mx,
+                                                    const unsigned int *cnt, int64_t cap) {
+    if ((int64_t)*cnt <= cap) return;
     const int r = blockIdx.y, lane = threadIdx.x & 63;
     const int64_t N = k.N, H = N / 2;
     const float band = fmaxf(1e-3f, 3e-5f * __uint_as_float(mx[r]));
-    const double ramp = (double)k.p.ramp[r] * 5.421010862427522e-20;     // 2^-64
-    const double nyq = (double)k.p.nyq_im[r];
     const int64_t nw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);       // this wave's 64 samples
     const int64_t n = nw * 64 + lane;
-    cf *z = W1 + (int64_t)r * N;
-    const bool cand = n < N && fabsf(z[n < N ? n : 0].y - 1.0f) < band;
-    uint64_t todo = __ballot(cand);
+    cf *z = W1 + (int64_t)r * k.N;
+    uint64_t todo = __ballot(refine_cand(z, n, k.N, band));
     while (todo) {
         const int src = __ffsll((long long)todo) - 1;
         todo &= todo - 1;
         const int64_t ns = nw * 64 + src;
-        // per-bin phase step (revolutions): n/N - s
-        double phi = (double)ns / (double)N - ramp;
-        phi -= floor(phi);
-        // lane's bins k = 1 + lane + 64 j, phasor e^{2 pi i k phi} by recurrence
-        double sn, cs, s64, c64;
-        sincospi(2.0 * phi * (double)(1 + lane), &sn, &cs);
-        sincospi(2.0 * phi * 64.0, &s64, &c64);
-        double acc = 0.0;
-        for (int64_t kb = 1 + lane; kb < H; kb += 64) {
-            const double2 b = B[kb];
-            acc = fma(b.x, cs, fma(-b.y, sn, acc));
-            const double t = cs * c64 - sn * s64;
-            sn = cs * s64 + sn * c64;
-            cs = t;
-        }
-        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-        if (lane == src) {
-            double m = B[0].x + 2.0 * acc;
-            if (2 * H == N) m += B[H].x * nyq * ((ns & 1) ? -1.0 : 1.0);
-            m /= (double)N;
-            z[ns].y = m > 1.0 ? 2.0f : 0.0f;
-        }
+        const double m = refine_mask(k, B, r, ns, lane);
+        if (lane == src) z[ns].y = m > 1.0 ? 2.0f : 0.0f;
     }
 }
 
@@ -3442,6 +3572,7 @@ struct WsLayout {
     int64_t bs_chirp, bs_bhat, bs_z;   // Bluestein: w [N] | Bhat [M] | Z [nb][M] (cf)
     int64_t odd_tw;                    // odd N: exp(+2 pi i j / (N - 1)), j < N - 1 (cf)
     int64_t rf_tw, rf_B, rf_mx;        // float64 null decisions: e^{2 pi i n/N} [N], B [N/2+1] (double2), row max [nchan]
+    int64_t rf_part, rf_list, rf_cnt;  // ... partial spectra [kBsParts][N/2+1] (double2), candidate list, its count
 };
 
 static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
@@ -3484,6 +3615,9 @@ static WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
             w.rf_tw = o; o += al256(N * 16);
             w.rf_B = o;  o += al256((N / 2 + 1) * 16);
             w.rf_mx = o; o += al256((int64_t)nchan * 4);
+            w.rf_part = o; o += al256((int64_t)kBsParts * (N / 2 + 1) * 16);
+            w.rf_list = o; o += al256(refine_cap(nchan, N) * 8);
+            w.rf_cnt = o;  o += 256;
         }
         if (smooth_split(N)) {
             // mixed-radix four-step (inside the same bytes: the direct path
@@ -4044,13 +4178,25 @@ static int launch_null_refine(KP &k, hipStream_t st) {
     }
     k_tw64<<<stream_grid(k.N, 1), dim3(256), 0, st>>>(k.N, tw);
     LAUNCHCHK();
-    k_null_bspec<<<dim3((unsigned)((k.N / 2 + 1 + 255) / 256)), dim3(256), 0, st>>>(box, k.N, tw, B);
+    double2 *part = reinterpret_cast<double2 *>(base + w.rf_part);
+    unsigned long long *list = reinterpret_cast<unsigned long long *>(base + w.rf_list);
+    unsigned int *cnt = reinterpret_cast<unsigned int *>(base + w.rf_cnt);
+    const int64_t K = k.N / 2 + 1, cap = refine_cap(k.p.nchan, k.N);
+    k_null_bspec<<<dim3((unsigned)((K + 255) / 256), (unsigned)kBsParts), dim3(256), 0, st>>>(box, k.N, tw, part);
+    LAUNCHCHK();
+    k_null_bsum<<<dim3((unsigned)((K + 255) / 256)), dim3(256), 0, st>>>(part, K, B);
     LAUNCHCHK();
     HIPCHK(hipMemsetAsync(mx, 0, (size_t)k.p.nchan * 4, st));
+    HIPCHK(hipMemsetAsync(cnt, 0, 4, st));
     k_row_absmax<<<dim3((unsigned)std::min<int64_t>(64, (k.N + 255) / 256), (unsigned)k.p.nchan), dim3(256), 0, st>>>(
         W1, k.N, mx);
     LAUNCHCHK();
-    k_null_refine<<<dim3((unsigned)((k.N + 255) / 256), (unsigned)k.p.nchan), dim3(256), 0, st>>>(k, W1, B, mx);
+    const dim3 gs((unsigned)((k.N + 255) / 256), (unsigned)k.p.nchan);
+    k_null_cands<<<gs, dim3(256), 0, st>>>(k, W1, mx, list, cnt, cap);
+    LAUNCHCHK();
+    k_null_refine_list<<<dim3(8192), dim3(256), 0, st>>>(k, W1, B, list, cnt, cap);
+    LAUNCHCHK();
+    k_null_refine<<<gs, dim3(256), 0, st>>>(k, W1, B, mx, cnt, cap);     // (overflow only)
     LAUNCHCHK();
     return PSS_OK;
 }

@@ -58,7 +58,10 @@ def test_workspace_sizes():
     a = lambda b: ((b + 255) // 256) * 256
     # even N <= 2^17 on the fallback paths: + the float64 null decisions'
     # e^{2 pi i n/N} [N] and box spectrum [N/2 + 1] (double2), row maxima [nchan]
-    f64 = lambda n, nc: a(n * 16) + a((n // 2 + 1) * 16) + a(nc * 4)
+    # (+ round 5: the box spectrum's 16 partial sums and the refine
+    # candidate list -- 1/8 of the samples + 64 Ki entries of 8 B -- and its count)
+    f64 = lambda n, nc: (a(n * 16) + a((n // 2 + 1) * 16) + a(nc * 4) + a(16 * (n // 2 + 1) * 16)
+                         + a(min(nc * n, nc * n // 8 + 65536) * 8) + 256)
     sp = 2 * 2 * 244 * 8 + 244 * 8                                   # fallback W1, W2, twiddles
     assert L.pss_workspace_bytes(2, 244) == a(sp) + f64(244, 2) + 1024   # row: 976 B, aligned
     # Bluestein fallback (N > 8192, 2 x 5003): W1 only (forward and inverse
