@@ -2977,40 +2977,32 @@ __global__ __launch_bounds__(256) void k_bs_col(KP k, BsArgs a) {
         const bool hasa = ra >= 0, hasb = rc < k.p.nchan;
         if (k.p.src == PSS_SRC_LOAD && k.p.null_mode != PSS_NULL_UNDELAYED && hasa && hasb) {
             // rows already on the device (shift_t, filter_rows, disperse of a
-            // made signal): every load issued before the first is used, as
-            // in the generic first pass; indices clamped, values zeroed
-            // arithmetically past N
-            constexpr int NJ = NH / 4;
+            // made signal): no draws, so one sample per item with lanes along
+            // the row (coalesced loads), every load issued before the first
+            // is used; indices clamped, values zeroed arithmetically past N
             const float *rowa = k.p.data + (int64_t)ra * k.p.ld, *rowb = rowa + k.p.ld;
-            float xa[NJ][4], xb[NJ][4];
-            cf wv[NJ][4];
+            float xa[NH], xb[NH];
+            cf wv[NH];
 #pragma unroll
-            for (int it = 0; it < NJ; ++it) {
+            for (int it = 0; it < NH; ++it) {
                 const int idx = tid + it * T;
-                const int64_t n = (int64_t)(idx / (B / 4)) * a.M2 + n20 + (idx % (B / 4)) * 4;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int64_t nc = n + i < a.N ? n + i : 0;
-                    xa[it][i] = rowa[nc];
-                    xb[it][i] = rowb[nc];
-                    wv[it][i] = a.chirp[nc];
-                }
+                const int64_t n = (int64_t)(idx / B) * a.M2 + n20 + (idx & (B - 1));
+                const int64_t nc = n < a.N ? n : 0;
+                xa[it] = rowa[nc];
+                xb[it] = rowb[nc];
+                wv[it] = a.chirp[nc];
             }
 #pragma unroll
-            for (int it = 0; it < NI / 4; ++it) {
+            for (int it = 0; it < NI; ++it) {
                 const int idx = tid + it * T;
-                const int b4 = (idx % (B / 4)) * 4, n1 = idx / (B / 4);
-                const int64_t n = (int64_t)n1 * a.M2 + n20 + b4;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    cf v = make_float2(0.f, 0.f);
-                    if (it < NJ) {
-                        const float f = n + i < a.N ? 1.0f : 0.0f;
-                        v = cmul(make_float2(xa[it][i], xb[it][i]), wv[it][i]);
-                        v = make_float2(v.x * f, v.y * f);
-                    }
-                    lds[Lds<L>::at(b4 + i, n1)] = v;
+                const int b = idx & (B - 1), n1 = idx / B;
+                cf v = make_float2(0.f, 0.f);
+                if (it < NH) {
+                    const float f = (int64_t)n1 * a.M2 + n20 + b < a.N ? 1.0f : 0.0f;
+                    v = cmul(make_float2(xa[it], xb[it]), wv[it]);
+                    v = make_float2(v.x * f, v.y * f);
                 }
+                lds[Lds<L>::at(b, n1)] = v;
             }
         } else
 #pragma unroll
@@ -3138,6 +3130,31 @@ __global__ __launch_bounds__(256) void k_bs_col(KP k, BsArgs a) {
         static_assert(B >= 4, "fused epilogue: 4-sample items");
         const int ra = 2 * r - k.poff, rc = ra + 1;
         const bool hasa = ra >= 0, hasb = rc < k.p.nchan;
+        if (!k.p.noise && k.p.null_mode != PSS_NULL_DELAYED && k.p.out_kind == PSS_OUT_NONE && hasa && hasb) {
+            // the epilogue is a plain store (shift_t, filter_rows, disperse
+            // of a made signal): one sample per item, lanes along the row
+            // (coalesced stores), the chirp of the NH items loaded as a batch
+            float *oa = k.p.data + (int64_t)ra * k.p.ld, *ob = oa + k.p.ld;
+            cf c1[NH];
+#pragma unroll
+            for (int it = 0; it < NH; ++it) {
+                const int idx = otid + it * T;
+                const int64_t pos = (int64_t)(idx / B) * a.M2 + n20 + (idx & (B - 1));
+                c1[it] = a.chirp[pos < a.N ? pos : 0];
+            }
+#pragma unroll
+            for (int it = 0; it < NH; ++it) {
+                const int idx = otid + it * T;
+                const int b = idx & (B - 1), k1 = idx / B;
+                const int64_t pos = (int64_t)k1 * a.M2 + n20 + b;
+                if (pos < a.N) {
+                    const cf v = cmul(lds[Lds<L>::at(b, k1)], c1[it]);
+                    oa[pos] = v.x * invN;
+                    ob[pos] = -v.y * invN;
+                }
+            }
+            return;
+        }
         const float msk[4] = {0.f, 0.f, 0.f, 0.f};
         // y = conj(conv w) / N back into the thread's own LDS entries first
         // (a small loop, unrolled: cw stays in registers; the epilogue loop
@@ -4141,6 +4158,10 @@ static int bs_filter_pair(const KP &k, BsArgs a, int64_t nb, int npairs, hipStre
         int rc = bs_col_any(k, a, rows, fused ? 3 : 0, st);
         if (!rc) rc = bs_row_any(k, a, rows, st);
         if (!rc) rc = bs_col_any(k, f, rows, 1, st);
+        // (the separation as its own kernel: fused into the inverse's first
+        // pass, which reads X_n and X_{N-n}, each sample computed both
+        // channels' ramps at its bin -- twice sep's ramp work at two
+        // workgroups per CU: 2.74 ms against 0.79 + 0.90 at 512 x (2^20 - 2))
         if (!rc) {
             k_bs_sep<<<dim3((unsigned)std::min<int64_t>((k.N / 2 + 256) / 256, 1024), (unsigned)rows), dim3(256), 0,
                        st>>>(k, const_cast<cf *>(a.src), a.ld, (int)r0);

@@ -3,7 +3,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R
 OUT=gpurun_out/r05/bs2; mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
-    -k "bluestein or filter_rows or shift_t or golden_replay or simulate or baseband or observe or shard" > $OUT/tests.log 2>&1
+    -k "bluestein or filter_rows or shift_t or golden_replay or simulate or baseband or observe or shard or fastpath or stats" > $OUT/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; grep -E "^FAILED|passed|failed|Error" $OUT/tests.log | tail -8
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python tools/bs_time.py > $OUT/bs_time.txt 2>&1 || exit $?
