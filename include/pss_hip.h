@@ -208,6 +208,10 @@ const char *pss_build_hash(void);
 /* PSS_FLAG_NULL_F32 keeps the packed (direct / Bluestein) paths' delayed-null
    decisions in fp32 (no float64 re-evaluation near the threshold).          */
 #define PSS_FLAG_NULL_F32 4
+/* PSS_FLAG_REFINE_PER_SAMPLE runs those float64 re-evaluations through the
+   per-sample kernel instead of the compacted candidate list (the list's
+   overflow path; test hook: both give the same bits).                      */
+#define PSS_FLAG_REFINE_PER_SAMPLE 8
 int pss_set_flags(int flags);
 int pss_last_error(char *buf, size_t n);
 

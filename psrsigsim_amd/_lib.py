@@ -18,6 +18,7 @@ OUT_NONE, OUT_F32, OUT_I8 = 0, 1, 2
 FLAG_NO_FAST = 1
 FLAG_DIRECT_DFT = 2
 FLAG_NULL_F32 = 4
+FLAG_REFINE_PER_SAMPLE = 8
 P_PULSE, P_BOX, P_REP, P_NOISE, P_TEST = 1, 2, 3, 4, 5
 KERNEL_KINDS = ("elementwise", "single_pass", "fourstep_colA", "fourstep_row", "fourstep_colC",
                 "fallback_dft", "null_fix")

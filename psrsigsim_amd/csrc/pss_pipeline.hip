@@ -4202,7 +4202,7 @@ static int launch_null_refine(KP &k, hipStream_t st) {
     double2 *part = reinterpret_cast<double2 *>(base + w.rf_part);
     unsigned long long *list = reinterpret_cast<unsigned long long *>(base + w.rf_list);
     unsigned int *cnt = reinterpret_cast<unsigned int *>(base + w.rf_cnt);
-    const int64_t K = k.N / 2 + 1, cap = refine_cap(k.p.nchan, k.N);
+    const int64_t K = k.N / 2 + 1, cap = (g_flags & PSS_FLAG_REFINE_PER_SAMPLE) ? 0 : refine_cap(k.p.nchan, k.N);
     k_null_bspec<<<dim3((unsigned)((K + 255) / 256), (unsigned)kBsParts), dim3(256), 0, st>>>(box, k.N, tw, part);
     LAUNCHCHK();
     k_null_bsum<<<dim3((unsigned)((K + 255) / 256)), dim3(256), 0, st>>>(part, K, B);

@@ -243,3 +243,43 @@ def test_fold_periods_full_c3_size(hip_lib):
     x[:, :nper * nbin] = one.repeat(nper)
     out = Backend(samprate=1.0, name="b").fold_periods(_Sig(x), None, nbin=nbin)
     np.testing.assert_array_equal(out.cpu().numpy(), (one.cpu().numpy().astype(np.float64) * nper)[None].repeat(2, 0).astype(np.float32))
+
+
+@pytest.mark.parametrize("fold", [True, False])
+def test_null_refine_list_equals_per_sample(fold, hip_lib):
+    """The float64 null decisions of the packed paths: the compacted candidate
+    list (four candidates per wave) and the per-sample kernel (the list's
+    overflow path, PSS_FLAG_REFINE_PER_SAMPLE) give the same bits -- C4's
+    fold-mode geometry with a null (Bluestein at 30720, dense candidates) and
+    a search-mode Bluestein length."""
+    import psrsigsim_amd as pss
+    from psrsigsim_amd import _lib
+    from psrsigsim_amd.signal import FilterBankSignal
+    from psrsigsim_amd.pulsar import Pulsar, GaussProfile
+    from psrsigsim_amd.ism import ISM
+    from psrsigsim_amd.telescope import telescope as T
+
+    def run():
+        pss.seed(31)
+        if fold:
+            sig = FilterBankSignal(1400, 400, Nsubband=6, sample_rate=F0_B1855 * 1024 * 1e-6, sublen=60.0, fold=True)
+            psr = Pulsar(1.0 / F0_B1855, 0.005, profiles=GaussProfile(0.5, 0.05, 1))
+            psr.make_pulses(sig, tobs=1800.0)
+            ISM().disperse(sig, 13.299393)
+        else:
+            sig = FilterBankSignal(1400, 400, Nsubband=5, fold=False)
+            psr = Pulsar(0.005, 1.0, profiles=GaussProfile(0.5, 0.05, 1))
+            psr.make_pulses(sig, tobs=(100002 + 0.5) * 20.48e-6)
+            ISM().disperse(sig, 30)
+        psr.null(sig, 0.1)
+        T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True)
+        return sig.data.cpu().numpy()
+
+    L = _lib.load()
+    a = run()
+    old = L.pss_set_flags(_lib.FLAG_REFINE_PER_SAMPLE)
+    try:
+        b = run()
+    finally:
+        L.pss_set_flags(old)
+    np.testing.assert_array_equal(a, b)
