@@ -2897,6 +2897,8 @@ struct BsArgs {
                        // for the fused pair runs' internal rows (rows of N = 2^20 - 2 would
                        // otherwise start 16 B off a line and split every segment in two)
     int r0;            // first channel (pair runs: pair) of this batch
+    int fastio;        // fused first / last passes may take the one-sample-per-item
+                       // forms on device-resident rows (0 under PSS_FLAG_NO_FAST)
     int mode;          // 0 forward DFT (+ delay ramp), 1 inverse DFT (/N), 2 Bhat build; pair runs:
                        // 3 inverse DFT's first pass (conj input), 4 forward DFT's last pass (X out)
 };
@@ -2975,7 +2977,7 @@ __global__ __launch_bounds__(256) void k_bs_col(KP k, BsArgs a) {
         static_assert(B >= 4, "fused source: 4-sample items");
         const int ra = 2 * r - k.poff, rc = ra + 1;
         const bool hasa = ra >= 0, hasb = rc < k.p.nchan;
-        if (k.p.src == PSS_SRC_LOAD && k.p.null_mode != PSS_NULL_UNDELAYED && hasa && hasb) {
+        if (a.fastio && k.p.src == PSS_SRC_LOAD && k.p.null_mode != PSS_NULL_UNDELAYED && hasa && hasb) {
             // rows already on the device (shift_t, filter_rows, disperse of a
             // made signal): no draws, so one sample per item with lanes along
             // the row (coalesced loads), every load issued before the first
@@ -3130,7 +3132,8 @@ __global__ __launch_bounds__(256) void k_bs_col(KP k, BsArgs a) {
         static_assert(B >= 4, "fused epilogue: 4-sample items");
         const int ra = 2 * r - k.poff, rc = ra + 1;
         const bool hasa = ra >= 0, hasb = rc < k.p.nchan;
-        if (!k.p.noise && k.p.null_mode != PSS_NULL_DELAYED && k.p.out_kind == PSS_OUT_NONE && hasa && hasb) {
+        if (a.fastio && !k.p.noise && k.p.null_mode != PSS_NULL_DELAYED && k.p.out_kind == PSS_OUT_NONE && hasa &&
+            hasb) {
             // the epilogue is a plain store (shift_t, filter_rows, disperse
             // of a made signal): one sample per item, lanes along the row
             // (coalesced stores), the chirp of the NH items loaded as a batch
@@ -4233,6 +4236,7 @@ static int run_bluestein(KP &k, hipStream_t st) {
     a.bhat = reinterpret_cast<const cf *>(base + w.bs_bhat);
     a.N = k.N;
     a.ld = k.N;
+    a.fastio = !(g_flags & PSS_FLAG_NO_FAST);
     a.M = g.M;
     a.M1 = g.M1;
     a.M2 = g.M2;

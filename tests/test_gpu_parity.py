@@ -283,3 +283,26 @@ def test_null_refine_list_equals_per_sample(fold, hip_lib):
     finally:
         L.pss_set_flags(old)
     np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("N", [10006, 100002, (1 << 20) - 2])
+def test_bluestein_fused_rows_fast_equals_generic(N, hip_lib):
+    """Bluestein pair mode on device-resident rows: the one-sample-per-item
+    first / last column passes (coalesced row loads and stores) give the bits
+    of the generic 4-sample-item passes (PSS_FLAG_NO_FAST); odd row count, so
+    the last pair (a lone row) takes the generic form in both runs."""
+    import torch
+    from psrsigsim_amd import _lib
+    from psrsigsim_amd.utils import shift_t
+    x = torch.rand((5, N), device="cuda", generator=torch.Generator(device="cuda").manual_seed(N))
+    s = np.linspace(-77.3, 1234.5, 5)
+    a = shift_t(x.clone(), s, dt=1.0)
+    L = _lib.load()
+    old = L.pss_set_flags(_lib.FLAG_NO_FAST)
+    try:
+        b = shift_t(x.clone(), s, dt=1.0)
+    finally:
+        L.pss_set_flags(old)
+    a = a.cpu().numpy() if hasattr(a, "cpu") else np.asarray(a)
+    b = b.cpu().numpy() if hasattr(b, "cpu") else np.asarray(b)
+    np.testing.assert_array_equal(a, b)
