@@ -2755,24 +2755,27 @@ __global__ __launch_bounds__(256) void k_null_cands(KP k, const cf *W1, const un
     }
 }
 
-// four candidates per wave: every bin's B_k load serves four phasor
-// recurrences (the candidates' independent chains), a quarter of the L2
-// traffic of one candidate per wave
+// four candidates per wave, sixteen per workgroup: the box spectrum goes
+// through LDS in 1024-bin tiles that the workgroup's 16 candidates share,
+// and every bin serves four phasor recurrences per wave (the candidates'
+// independent chains).  A lane's bins k = 1 + lane + 64 j in order, as the
+// per-sample kernel walks them.
 __global__ __launch_bounds__(256) void k_null_refine_list(KP k, cf *W1, const double2 *B,
                                                          const unsigned long long *list, const unsigned int *cnt,
                                                          int64_t cap) {
-    constexpr int C = 4;
-    const int lane = threadIdx.x & 63;
+    constexpr int C = 4, TB = 1024;
+    __shared__ double2 tile[TB];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t total = min((int64_t)*cnt, cap);
     const int64_t N = k.N, H = N / 2;
-    const int64_t nw = (int64_t)gridDim.x * 4;
-    for (int64_t e0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * C; e0 < total; e0 += nw * C) {
+    for (int64_t g0 = (int64_t)blockIdx.x * 16; g0 < total; g0 += (int64_t)gridDim.x * 16) {
+        const int64_t e0 = g0 + wv * C;
         int r[C];
         int64_t ns[C];
         double sn[C], cs[C], s64[C], c64[C], acc[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            const int64_t e = e0 + c < total ? e0 + c : e0;           // (a repeat of e0: not written)
+            const int64_t e = e0 + c < total ? e0 + c : g0;           // (a repeat of g0: not written)
             const unsigned long long v = list[e];
             r[c] = (int)(v >> 32);
             ns[c] = (int64_t)(v & 0xffffffffull);
@@ -2782,14 +2785,21 @@ __global__ __launch_bounds__(256) void k_null_refine_list(KP k, cf *W1, const do
             sincospi(2.0 * phi * 64.0, &s64[c], &c64[c]);
             acc[c] = 0.0;
         }
-        for (int64_t kb = 1 + lane; kb < H; kb += 64) {
-            const double2 b = B[kb];
+        for (int64_t base = 1; base < H; base += TB) {
+            __syncthreads();                                  // the previous tile is consumed
+            for (int i = threadIdx.x; i < TB; i += 256)
+                tile[i] = base + i < H ? B[base + i] : make_double2(0.0, 0.0);
+            __syncthreads();
+            const int cntb = (int)min((int64_t)TB, H - base);
+            for (int i = lane; i < cntb; i += 64) {
+                const double2 b = tile[i];
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                acc[c] = fma(b.x, cs[c], fma(-b.y, sn[c], acc[c]));
-                const double t = cs[c] * c64[c] - sn[c] * s64[c];
-                sn[c] = cs[c] * s64[c] + sn[c] * c64[c];
-                cs[c] = t;
+                for (int c = 0; c < C; ++c) {
+                    acc[c] = fma(b.x, cs[c], fma(-b.y, sn[c], acc[c]));
+                    const double t = cs[c] * c64[c] - sn[c] * s64[c];
+                    sn[c] = cs[c] * s64[c] + sn[c] * c64[c];
+                    cs[c] = t;
+                }
             }
         }
 #pragma unroll
@@ -4218,7 +4228,7 @@ static int launch_null_refine(KP &k, hipStream_t st) {
     const dim3 gs((unsigned)((k.N + 255) / 256), (unsigned)k.p.nchan);
     k_null_cands<<<gs, dim3(256), 0, st>>>(k, W1, mx, list, cnt, cap);
     LAUNCHCHK();
-    k_null_refine_list<<<dim3(8192), dim3(256), 0, st>>>(k, W1, B, list, cnt, cap);
+    k_null_refine_list<<<dim3(4096), dim3(256), 0, st>>>(k, W1, B, list, cnt, cap);
     LAUNCHCHK();
     k_null_refine<<<gs, dim3(256), 0, st>>>(k, W1, B, mx, cnt, cap);     // (overflow only)
     LAUNCHCHK();
