@@ -430,6 +430,7 @@ class PowerSampler:
         self.samples = []
         self.limit_w = None
         self._stop = threading.Event()
+        self._ready = threading.Event()
         self._thread = None
         try:
             import amdsmi
@@ -452,20 +453,32 @@ class PowerSampler:
         except Exception:
             self._thread = None
 
+    def _sample(self):
+        try:
+            w = self._smi.amdsmi_get_power_info(self._h).get("current_socket_power")
+            c = self._smi.amdsmi_get_clock_info(self._h, self._smi.AmdSmiClkType.GFX).get("clk")
+            if isinstance(w, (int, float)) and isinstance(c, (int, float)):
+                self.samples.append((float(w), float(c)))
+            return True
+        except Exception:
+            return False
+
     def _run(self, period):
-        while not self._stop.is_set():
-            try:
-                w = self._smi.amdsmi_get_power_info(self._h).get("current_socket_power")
-                c = self._smi.amdsmi_get_clock_info(self._h, self._smi.AmdSmiClkType.GFX).get("clk")
-                if isinstance(w, (int, float)) and isinstance(c, (int, float)):
-                    self.samples.append((float(w), float(c)))
-            except Exception:
+        self._ready.set()
+        while not self._stop.wait(period):
+            if not self._sample():
                 return
-            self._stop.wait(period)
 
     def start(self):
+        """A sample every `period` s on the thread, the first one `period`
+        after the start; returns once the thread waits for it.  amdsmi calls
+        slow the host work of the next ~2 ms (C4's first timed step: 1.9-2.1
+        ms after amdsmi_init or a sample right before it, 1.1-1.2 without;
+        profiles/r05/power_sampler.txt), so the sampler is built before the
+        warm-up and takes no sample at the start of the timed region."""
         if self._thread is not None:
             self._thread.start()
+            self._ready.wait(1.0)
 
     def stop(self):
         if self._thread is not None:
@@ -629,6 +642,7 @@ def main():
             return tutorial_step(pss, args.workload, total, shard, plan_group=pg)
         return c3_step(pss, total, shard, args.log2n, plan_group=pg)
 
+    power = None if args.dry_run else PowerSampler(torch.cuda.current_device())
     for _ in range(args.warmup):
         s = step()
         del s
@@ -644,10 +658,9 @@ def main():
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         for e in evs:
             e.record()
-    power = None if args.dry_run else PowerSampler(torch.cuda.current_device())
-    barrier()
     if power is not None:
         power.start()
+    barrier()
     t0 = time.perf_counter()
     if evs:
         evs[0].record()
