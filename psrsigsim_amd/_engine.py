@@ -110,7 +110,16 @@ def device():
 
 
 def stream_ptr():
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    """The launch stream for a library call; it first waits (on the device)
+    for the uploads to_dev queued since the last call -- one event per call,
+    not one per table."""
+    st = torch.cuda.current_stream()
+    if _upload_pending:
+        idx = st.device.index
+        if idx in _upload_pending:
+            st.wait_stream(_upload[idx])
+            _upload_pending.discard(idx)
+    return ctypes.c_void_p(st.cuda_stream)
 
 
 _ws = {}
@@ -136,15 +145,48 @@ def release_workspace():
     _ws.clear()
 
 
+_upload = {}
+_upload_pending = set()
+# "stream": every upload on the upload stream; "direct": on the launch stream;
+# "auto": the upload stream after a large run (>= 2^27 channel-samples: what a
+# stall would wait for is long), the launch stream after a small one (C4's
+# 0.5-ms steps: the cross-stream event cost more than a stall, 0.565 vs 0.503
+# ms/step; 256 x 2^22: 6.83 against 7.07 direct; tools/ab_upload.py)
+UPLOAD_MODE = "auto"
+_UPLOAD_STREAM_MIN = 1 << 27
+_last_run = [0]
+
+
 def to_dev(a, dtype=None):
     """Host array -> device tensor, stream-ordered and without blocking the
-    host: from pageable memory the copy would wait for the stream to drain
+    host.  From pageable memory the copy would wait for the stream to drain
     (i.e. for the previous signal's fused run), so it goes through a pinned
-    staging copy (torch's caching host allocator) and a non-blocking copy."""
+    staging copy (torch's caching host allocator).  And it runs on an upload
+    stream of its own, the launch stream waiting for it on the device: a
+    small "asynchronous" copy on the launch stream itself still blocked the
+    host until that stream drained, now and then (a whole step's kernels,
+    ~7 ms at 256 channels x 2^22, during which the next step's planning could
+    not run -- tools/host_stalls.py, tools/r5_hiptrace.sh).  The destination
+    comes from the upload stream's pool, so it never aliases memory the
+    launch stream still uses, and is recorded on the launch stream before it
+    returns to the pool.  The launch stream waits for the upload stream at
+    the next library call (stream_ptr), once for all of a run's tables."""
     t = torch.as_tensor(np.ascontiguousarray(a))
     if dtype is not None:
         t = t.to(dtype)
-    return t.pin_memory().to(device(), non_blocking=True)
+    t = t.pin_memory()
+    dev = device()
+    main = torch.cuda.current_stream(dev)
+    if UPLOAD_MODE == "direct" or (UPLOAD_MODE == "auto" and _last_run[0] < _UPLOAD_STREAM_MIN):
+        return t.to(dev, non_blocking=True)
+    up = _upload.get(dev.index)
+    if up is None:
+        up = _upload[dev.index] = torch.cuda.Stream(dev)
+    with torch.cuda.stream(up):
+        d = t.to(dev, non_blocking=True)
+    d.record_stream(main)
+    _upload_pending.add(dev.index)
+    return d
 
 
 def ptr(t):
@@ -334,6 +376,10 @@ def build_pipeline(sig, pend, rows, chan0, data, out=None, ws_role="main"):
 def run(p, keep):
     rc = _lib.lib().pss_run(ctypes.byref(p), stream_ptr())
     _lib.check(rc, "pss_run")
+    # (to_dev's upload-stream choice: the size of the recent runs, decaying
+    # by half per smaller run, so null()'s 2-channel probe between two band
+    # runs does not count as "small")
+    _last_run[0] = max(int(p.nchan) * int(p.nsamp), _last_run[0] // 2)
     return keep
 
 
