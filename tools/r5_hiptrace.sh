@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r05/hiptrace; rm -rf $OUT; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --hip-trace --output-format csv -d $OUT/raw -o h -- \
-    python3 $R/tools/host_stalls.py 256 30 > $OUT/log.txt 2>&1 || { tail -5 $OUT/log.txt; exit 1; }
+    python3 $R/tools/host_stalls.py 256 60 > $OUT/log.txt 2>&1 || { tail -5 $OUT/log.txt; exit 1; }
 grep -E "median|step" $OUT/log.txt
 f=$(find $OUT/raw -name "*hip_api_trace.csv" | head -1)
 python3 - "$f" <<'PY'
