@@ -40,11 +40,14 @@ inline double edge_slope(double h0, double h1, double m0, double m1) {
 
 template <typename F>
 void parallel_rows(int64_t rows, int nthreads, F fn) {
-    if (nthreads <= 1 || rows < 64) {
+    if (nthreads <= 1 || rows < 512) {
         fn(0, rows);
         return;
     }
-    const int nt = (int)std::min<int64_t>(nthreads, rows / 32);
+    // >= 256 rows per thread: a thread costs ~50-100 us to start and join,
+    // more than a 256-row share of these passes (make_pulses at 256 channels
+    // x 244 phases: 3.3 ms on one thread, 5.7 on eight, this container)
+    const int nt = (int)std::min<int64_t>(nthreads, rows / 256);
     std::vector<std::thread> th;
     th.reserve(nt);
     for (int t = 0; t < nt; ++t) {
