@@ -1,6 +1,6 @@
 """Host time of each API call of the C3 step (bench.c3_step's sequence) on
 an idle GPU -- the first timed step's exposed planning, call by call.
-GPU box.  usage: tools/host_calls.py [nchan ...]"""
+GPU box.  usage: tools/host_calls.py [c4] [nchan ...]   (c4: bench.c4_step's sequence)"""
 import os
 import sys
 import time
@@ -36,8 +36,30 @@ def step(nch, t):
     return sig
 
 
+def step_c4(nch, t):
+    from psrsigsim_amd.pulsar import DataProfile
+    t.append(time.perf_counter())
+    sig = FilterBankSignal(1400, 400, Nsubband=nch, sample_rate=bench.F0_B1855 * 1024 * 1e-6, sublen=60.0,
+                           fold=True)
+    psr = Pulsar(1.0 / bench.F0_B1855, 0.005, profiles=DataProfile(bench.b1855_profile(), Nchan=nch))
+    t.append(time.perf_counter())
+    t.append(time.perf_counter())
+    psr.make_pulses(sig, tobs=1800.0)
+    t.append(time.perf_counter())
+    ISM().disperse(sig, 13.299393)
+    t.append(time.perf_counter())
+    t.append(time.perf_counter())
+    T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True)
+    t.append(time.perf_counter())
+    return sig
+
+
 names = ["construct", "scatter_broaden", "make_pulses", "disperse", "null", "observe(launch)"]
-for nch in [int(a) for a in sys.argv[1:]] or [256, 2048]:
+args = sys.argv[1:]
+if args and args[0] == "c4":
+    step = step_c4
+    args = args[1:]
+for nch in [int(a) for a in args] or [256, 2048]:
     for _ in range(2):
         step(nch, [])
     torch.cuda.synchronize()
