@@ -147,13 +147,23 @@ class ISM(object):
             if getattr(pulsar.Profiles, "_rowset", None) is not rs:
                 full_profs = full_profs[rs.gids]
             full_profs = np.array(full_profs)
-            tails = np.exp(-(t[None, :] * 1e3) / tau[rs.gids][:, None])
-            pulsar._Profiles = DataPortrait(self.convolve_profile(full_profs, tails, width=Nph), rowset=rs)
+            taur = tau[rs.gids]
+            pulsar._Profiles = DataPortrait(self._convolve_rows(
+                full_profs, lambda a, b: np.exp(-(t[None, :] * 1e3) / taur[a:b, None]), Nph), rowset=rs)
             return
         full_profs = np.array(full_profs)      # convolved per channel (a uniform table no longer is)
-        tails = np.zeros((signal.Nchan, Nph))
-        tails[:tau.size, :] = np.exp(-(t[None, :] * 1e3) / tau[:, None])   # t [s] / tau [ms]
-        pulsar._Profiles = DataPortrait(self.convolve_profile(full_profs, tails, width=Nph))
+
+        def tails(a, b):
+            # rows [a, b) of the exponential tails, t [s] / tau [ms]; rows past
+            # tau.size zero (the reference's tails[:tau.size]); computed on
+            # the convolution's row-block threads, elementwise as one array
+            k = np.zeros((b - a, Nph))
+            e = min(b, tau.size)
+            if e > a:
+                k[:e - a, :] = np.exp(-(t[None, :] * 1e3) / tau[a:e, None])
+            return k
+
+        pulsar._Profiles = DataPortrait(self._convolve_rows(full_profs, tails, Nph))
 
     def convolve_profile(self, profiles, convolve_array, width=2048):
         """ism.py:243-288: per row, linear convolution of the sum-normalised
@@ -161,15 +171,22 @@ class ISM(object):
         rescaled by the profile sum.  Row blocks run on host threads (every
         step is row-wise: numpy and pocketfft release the GIL), so the
         per-signal planning of a 2048-channel band is not one core's work."""
-        prof = np.asarray(profiles, dtype=float)
         kern = np.asarray(convolve_array, dtype=float)
-        rows = kern.shape[0]
+        return self._convolve_rows(profiles, lambda a, b: kern[a:b], width, rows=kern.shape[0])
+
+    def _convolve_rows(self, profiles, kern_rows, width, rows=None):
+        """convolve_profile with the kernel rows [a, b) from ``kern_rows(a,
+        b)``, so scatter_broaden's tails are computed on the row-block
+        threads too (bit for bit the same values)."""
+        prof = np.asarray(profiles, dtype=float)
+        rows = prof.shape[0] if rows is None else rows
 
         def block(a, b):
+            kb = kern_rows(a, b)
             ps = np.sum(prof[a:b], axis=1, keepdims=True)
             pn = np.where(ps != 0.0, prof[a:b] / np.where(ps != 0.0, ps, 1.0), prof[a:b])
-            ks = np.sum(kern[a:b], axis=1, keepdims=True)
-            kn = np.where(ks != 0.0, kern[a:b] / np.where(ks != 0.0, ks, 1.0), kern[a:b])
+            ks = np.sum(kb, axis=1, keepdims=True)
+            kn = np.where(ks != 0.0, kb / np.where(ks != 0.0, ks, 1.0), kb)
             # scipy's FFT convolution batched over rows: bit-identical to the
             # reference's per-row scipy.signal.convolve(..., method='fft')
             # (the reference later makes exact float decisions on these values)
