@@ -323,6 +323,15 @@ def dry_step(pss, nchan_total, shard, nsamp_log2, plan_group=None):
     return sig
 
 
+def usable_cores():
+    """CPUs this process may run on (its affinity set: the box's share of a
+    many-core host), next to os.cpu_count() (the whole machine)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count()
+
+
 def cpu_baseline(nch, nsamp_log2):
     """The oracle (NumPy restatement with the reference's call structure:
     per-channel rfft/irfft, legacy RandomState chi2, scipy PCHIP), single
@@ -774,12 +783,12 @@ def main():
         if args.cpu_workers > 0:
             va, dta = cpu_baseline_allcore(args.cpu_workers, 2, args.log2n)
             cpu_all = {"value": round(va, 1), "unit": "channel-samples/s", "cores": args.cpu_workers,
-                       "cpu_count": os.cpu_count(), "kind": "port",
+                       "cpu_count": os.cpu_count(), "usable_cores": usable_cores(), "kind": "port",
                        "sample": "%d concurrent single-threaded processes x 2 ch x 2^%d samp of the same C3 "
                                  "pipeline (oracle/pss_cpu.py), slowest worker %.1f s" % (args.cpu_workers,
                                                                                          args.log2n, dta)}
         cpu = {"value": round(v, 1), "unit": "channel-samples/s", "cores": 1, "cpu_count": os.cpu_count(),
-               "kind": "port",
+               "usable_cores": usable_cores(), "kind": "port",
                "sample": "%d ch x 2^%d samp of the same C3 pipeline, oracle/pss_cpu.py (float64 NumPy, "
                          "reference call structure; like the reference it also builds observe's pre-noise "
                          "out copy, ~2%% of its time, which the GPU run elides when ret_resampsig=False), "
@@ -798,8 +807,8 @@ def main():
             c = cpu_tutorial(args.workload, total)
             tut["cpu_oracle"] = {"disperse_only": round(c["disperse"], 1), "disperse_s": round(c["disperse_s"], 3),
                                  "pipeline": round(c["pipeline"], 1), "pipeline_s": round(c["pipeline_s"], 3),
-                                 "cores": 1, "cpu_count": os.cpu_count(), "kind": "port",
-                                 "host": cpu_model()}
+                                 "cores": 1, "cpu_count": os.cpu_count(), "usable_cores": usable_cores(),
+                                 "kind": "port", "host": cpu_model()}
             tut["gpu_disperse_only"]["vs_cpu_oracle"] = round(gv / c["disperse"], 1)
     if rank == 0:
         line = {
@@ -813,6 +822,8 @@ def main():
             "gpu_kernel_ms_per_step": round(gpu_ms, 3),
             "step_ms_first": round(spans[0], 3) if spans else None,
             "step_ms_steady": round(float(np.median(spans[1:])), 3) if len(spans) > 1 else None,
+            "step_ms_first_minus_steady": (round(spans[0] - float(np.median(spans[1:])), 3)
+                                           if len(spans) > 1 else None),
             "gpu_power": power.report() if power is not None else None,
             "kernels": kernels,
             "roofline": roof,

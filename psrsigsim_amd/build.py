@@ -11,11 +11,16 @@ import os
 import re
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = [os.path.join(HERE, "csrc", "pss_pipeline.hip"), os.path.join(HERE, "csrc", "pss_host.cpp")]
-DEPS = SRC + [os.path.join(HERE, "csrc", f) for f in ("pss_device.hpp", "pss_fft.hpp")] + \
+# launch units: one translation unit each (the kernel templates are
+# instantiated per unit), compiled in parallel and linked with the host code
+UNITS = ["pss_pipeline.hip", "pss_fourstep.hip", "pss_fourstep_b.hip", "pss_smooth.hip", "pss_smooth_b.hip",
+         "pss_smooth_c.hip", "pss_single.hip", "pss_fallback.hip"]
+SRC = [os.path.join(HERE, "csrc", u) for u in UNITS] + [os.path.join(HERE, "csrc", "pss_host.cpp")]
+DEPS = SRC + [os.path.join(HERE, "csrc", f) for f in ("pss_engine.hpp", "pss_device.hpp", "pss_fft.hpp")] + \
     [os.path.join(ROOT, "include", "pss_hip.h")]
 OUT = os.path.join(HERE, "libpss_hip.so")
 OUT_DEBUG = os.path.join(HERE, "libpss_hip_debug.so")
@@ -65,11 +70,25 @@ def build(force=False, verbose=True, debug=False):
     if not force and embedded_hash(out) == source_hash(extra):
         return out
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc] + FLAGS + extra + ['-DPSS_BUILD_HASH="%s"' % source_hash(extra),
-                                     "-I" + os.path.join(ROOT, "include"), "-o", out + ".tmp"] + SRC
+    objdir = os.path.join(HERE, "build", "debug" if debug else "release")
+    os.makedirs(objdir, exist_ok=True)
+    defs = extra + ['-DPSS_BUILD_HASH="%s"' % source_hash(extra), "-I" + os.path.join(ROOT, "include")]
+    cflags = [f for f in FLAGS if f != "-shared"]
+    jobs = []
+    for src in SRC[:-1]:
+        obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
+        jobs.append(([hipcc] + cflags + defs + ["-c", "-o", obj, src], obj))
     if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+        print("compiling %d units in parallel: %s" % (len(jobs), " ".join(jobs[0][0][:-3])), file=sys.stderr)
+    workers = max(1, min(len(jobs), os.cpu_count() or 4, 16))
+    with ThreadPoolExecutor(workers) as ex:
+        results = list(ex.map(lambda j: subprocess.run(j[0], capture_output=True, text=True), jobs))
+    for (cmd, _), r in zip(jobs, results):
+        if r.returncode != 0:
+            sys.stderr.write(r.stdout + r.stderr)
+            raise subprocess.CalledProcessError(r.returncode, cmd)
+    link = [hipcc] + FLAGS + defs + ["-o", out + ".tmp"] + [o for _, o in jobs] + [SRC[-1]]
+    subprocess.run(link, check=True, capture_output=not verbose)
     os.replace(out + ".tmp", out)
     return out
 

@@ -83,9 +83,31 @@ def test_fused_resampled_out_int8(hip_lib):
         ref = np.stack([O.down_sample(row, kind[1]) for row in pre])
     else:
         ref = np.stack([O.rebin(row, kind[1]) for row in pre])
-    ref = np.minimum(ref, 127.0).astype(np.int8)
+    mean = np.minimum(ref, 127.0)
+    ref = mean.astype(np.int8)
     got = out.cpu().numpy()
-    # fp32 data against the float64 means: a mean within 1e-5 relative of an
-    # integer may truncate either way
+    # the device sums the same fp32 samples (fp32 pieces, float64 windows) and
+    # truncates its float64 mean directly: exact wherever the oracle's mean
+    # is not within the fp32 summation error of an integer
+    # (the int8 signal's samples are small integers, so window means at or
+    # next to an integer are common: ~1.6 % here)
+    near = np.abs(mean - np.round(mean)) <= 1e-5 * np.maximum(np.abs(mean), 1.0)
+    np.testing.assert_array_equal(got[~near], ref[~near])
     d = np.abs(got.astype(np.int64) - ref.astype(np.int64))
     assert d.max() <= 1 and (d > 0).mean() < 1e-3
+
+
+@pytest.mark.parametrize("N,factor", [(1 << 16, 2.5), (1 << 20, 64.0)])
+def test_fused_resampled_out_repeatable(N, factor, hip_lib):
+    """The window sums leave each wave as float64 atomics whose order is the
+    hardware's (pss_pipeline.hip out_windows): the pieces are fp32 sums of
+    one row's samples, so the float64 additions are exact unless a window
+    mixes pieces ~2^29 apart in magnitude, and a last-bit difference in the
+    float64 mean survives the cast to float32 only at a rounding boundary.
+    Two identical runs must give the same resampled bits."""
+    outs = []
+    for _ in range(2):
+        _, out, kind = _run(N, 2, 30, factor, ret=True, noise=True, seed=4242)
+        assert kind[0] in ("down", "rebin"), kind
+        outs.append(out.cpu().numpy())
+    np.testing.assert_array_equal(outs[0], outs[1])

@@ -3,7 +3,7 @@
 
 usage: isa_mix.py ASM_FILE NAME_SUBSTRING [...]
 (ASM_FILE: hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-slp-vectorize
- --cuda-device-only -S -o pss.s psrsigsim_amd/csrc/pss_pipeline.hip)
+ --cuda-device-only -S -o pss.s psrsigsim_amd/csrc/pss_fourstep.hip: the C3 kernels; other units for the other paths)
 
 For each matching kernel: the per-class count of the (fully unrolled)
 kernel body, per phase (the code between workgroup barriers) and in total,

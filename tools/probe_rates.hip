@@ -46,6 +46,12 @@ K(k_add, float, (float)(seed + threadIdx.x + c), asm volatile("v_add_f32 %0, %0,
   (uint32_t)a[c])
 K(k_pkfma, float2, make_float2(seed + threadIdx.x + c, c),
   asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(a[c]) : "v"(make_float2(seed, seed))), (uint32_t)(a[c].x + a[c].y))
+K(k_pkadd, float2, make_float2(seed + threadIdx.x + c, c),
+  asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(a[c]) : "v"(make_float2(seed, seed))), (uint32_t)(a[c].x + a[c].y))
+K(k_pkmul, float2, make_float2(seed + threadIdx.x + c, c),
+  asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(a[c]) : "v"(make_float2(1.0f, 1.0f))), (uint32_t)(a[c].x + a[c].y))
+K(k_mul, float, (float)(seed + threadIdx.x + c), asm volatile("v_mul_f32 %0, %0, %1" : "+v"(a[c]) : "v"(1.0f)),
+  (uint32_t)a[c])
 K(k_mul_lo, uint32_t, seed + threadIdx.x + c, asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[c]) : "v"(seed)), a[c])
 K(k_mul_hi, uint32_t, seed + threadIdx.x + c, asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[c]) : "v"(seed)), a[c])
 K(k_mad64, uint64_t, seed + threadIdx.x + c,
@@ -79,6 +85,7 @@ int main() {
     hipEventCreate(&eb);
     struct { const char *n; KF f; } ks[] = {
         {"v_fma_f32", k_fma},       {"v_fma_f32 (a,s,s)", k_fma_same}, {"v_add_f32", k_add},         {"v_pk_fma_f32", k_pkfma},
+        {"v_pk_add_f32", k_pkadd},  {"v_pk_mul_f32", k_pkmul},   {"v_mul_f32", k_mul},
         {"v_mul_lo_u32", k_mul_lo}, {"v_mul_hi_u32", k_mul_hi},   {"v_mad_u64_u32", k_mad64},
         {"v_mul_u32_u24", k_mul24}, {"v_mul_hi_u32_u24", k_mulhi24}, {"v_xor_b32", k_xor},
         {"v_bitop3_b32", k_bitop3}, {"v_sin_f32", k_sin},         {"v_log_f32", k_log},

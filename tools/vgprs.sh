@@ -1,7 +1,9 @@
 #!/bin/bash
-# Compile the pipeline for gfx950 and list VGPRs / occupancy / scratch per kernel.
-cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-slp-vectorize -c -I/root/repo/include \
-  /root/repo/psrsigsim_amd/csrc/pss_pipeline.hip -o /tmp/vg.o -Rpass-analysis=kernel-resource-usage "$@" 2>&1 | \
+# Compile one launch unit for gfx950 and list VGPRs / occupancy / scratch per kernel.
+# usage: tools/vgprs.sh [UNIT] [extra hipcc flags]   (UNIT default pss_fourstep.hip: the C3 kernels)
+U=${1:-pss_fourstep.hip}; shift
+cd /tmp && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fno-slp-vectorize -ffp-contract=on -c \
+  -I/root/repo/include /root/repo/psrsigsim_amd/csrc/$U -o /tmp/vg.o -Rpass-analysis=kernel-resource-usage "$@" 2>&1 | \
 python3 -c '
 import sys, re
 cur = None
