@@ -215,6 +215,14 @@ const char *pss_build_hash(void);
 int pss_set_flags(int flags);
 int pss_last_error(char *buf, size_t n);
 
+/* Launch-plan log (test hook): the kernels every pss_run since the last call
+ * picked, one line per run -- "<nchan>x<nsamp>: <path> <split> A:<pass A>
+ * R:<row pass> C:<pass C> N:<null>", e.g. "2048x4194304: fourstep 1024x4096
+ * A:fast R:pair_row C:fast N:table N:fix_list" -- copied into buf (up to n - 1
+ * bytes, NUL-terminated); returns the log's length and clears it.  The parity
+ * tests assert with it which kernels produced the bits they check.        */
+int pss_plan_collect(char *buf, size_t n);
+
 /* Opt-in kernel timing for benchmarks: while enabled, pss_run records a pair
  * of hipEvents on its stream around every kernel it launches.  collect()
  * synchronises on them and returns, per launch (up to `cap`), the kernel kind

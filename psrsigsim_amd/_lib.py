@@ -55,6 +55,7 @@ EXPORTS = {
     "pss_build_hash": (ctypes.c_char_p, []),
     "pss_set_flags": (ctypes.c_int, [ctypes.c_int]),
     "pss_last_error": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
+    "pss_plan_collect": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
     "pss_workspace_bytes": (c_i64, [c_i32, c_i64]),
     "pss_timing_enable": (None, [ctypes.c_int]),
     "pss_timing_span_ms": (ctypes.c_double, []),
@@ -135,6 +136,14 @@ def timing_collect(cap=4096):
     u = (c_i64 * cap)()
     n = load().pss_timing_collect(k, ms, u, cap)
     return [(KERNEL_KINDS[k[i]], ms[i], u[i]) for i in range(n)]
+
+
+def plan_collect():
+    """The launch-plan lines of the pss_run calls since the last collect
+    (pss_plan_collect: which kernels each run picked), and clear them."""
+    buf = ctypes.create_string_buffer(16384)
+    load().pss_plan_collect(buf, 16384)
+    return [l for l in buf.value.decode(errors="replace").split("\n") if l]
 
 
 def last_error():

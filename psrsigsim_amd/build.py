@@ -61,16 +61,21 @@ def stale():
     return embedded_hash() != source_hash()
 
 
-def build(force=False, verbose=True, debug=False):
+def build(force=False, verbose=True, debug=False, variant=None, variant_flags=()):
     """Build the product library, or with ``debug=True`` the device-assert
     build ``libpss_hip_debug.so`` (PSS_DEBUG=1: bounds asserts on generic and
     buffer accesses; load it with PSS_LIB_PATH, tools/debug_gpu.sh)."""
     extra = ["-DPSS_DEBUG=1"] if debug else []
     out = OUT_DEBUG if debug else OUT
+    if variant:
+        # an A/B build (tools/r3_abn.sh loads it through PSS_LIB_PATH): the
+        # product sources with extra compile flags, e.g. -D switches
+        extra = list(variant_flags)
+        out = os.path.join(HERE, "libpss_hip_%s.so" % variant)
     if not force and embedded_hash(out) == source_hash(extra):
         return out
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    objdir = os.path.join(HERE, "build", "debug" if debug else "release")
+    objdir = os.path.join(HERE, "build", variant or ("debug" if debug else "release"))
     os.makedirs(objdir, exist_ok=True)
     defs = extra + ['-DPSS_BUILD_HASH="%s"' % source_hash(extra), "-I" + os.path.join(ROOT, "include")]
     cflags = [f for f in FLAGS if f != "-shared"]
@@ -94,4 +99,9 @@ def build(force=False, verbose=True, debug=False):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, debug="--debug" in sys.argv)
+    # python -m psrsigsim_amd.build [--force] [--debug] [--variant NAME FLAG ...]
+    if "--variant" in sys.argv:
+        i = sys.argv.index("--variant")
+        build(force=True, variant=sys.argv[i + 1], variant_flags=sys.argv[i + 2:])
+    else:
+        build(force="--force" in sys.argv, debug="--debug" in sys.argv)

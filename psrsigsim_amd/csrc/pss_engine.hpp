@@ -60,6 +60,10 @@ int fail(int code, const char *fmt, ...);
 enum { TK_ELEM = 0, TK_SINGLE, TK_COLA, TK_ROW, TK_COLC, TK_FALLBACK, TK_NULLFIX, TK_N };
 void tk_begin(int kind, hipStream_t st);
 void tk_end(hipStream_t st);
+// launch-plan log (pss_plan_collect): every launch path notes the kernels it
+// picked ("fourstep 1024x4096 A:fast R:pair_row C:fast N:fix_list"), so the
+// parity tests can assert which kernels produced the bits they check
+void plan_note(const char *fmt, ...);
 
 // ---------------------------------------------------------------------------
 // kernel parameters
@@ -2241,6 +2245,7 @@ template <int L, int BATCH, int T, typename F, typename I>
 static int launch_single(const KP &k, hipStream_t st) {
     using SP = SinglePass<L, BATCH, T, F, I>;
     dim3 grid((k.p.nchan + BATCH - 1) / BATCH);
+    plan_note("single %d", L);
     tk_begin(TK_SINGLE, st);
     k_single<SP, T><<<grid, dim3(T), 0, st>>>(k);
     tk_end(st);
@@ -2503,6 +2508,7 @@ static inline int build_mask_table(KP &k, hipStream_t st, const float *mask_row,
         k.nwlist = wcount;
     }
     k.mtab = 1;
+    plan_note(" N:table");
     k.log2n = log2n;
     if (k.p.data_in_fft && !fast_epilogue(k)) {   // generic pass C reads the decisions as bits
         k.mbB = B;
@@ -2547,6 +2553,7 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
     using PC = PairCols<N1, B, T, CF, CI, xrs_read(B)>;
     using PCC = PairCols<N1, BC, TC, CF, CI, xrs_write(BC)>;
     using PR = PairRows<N2, TR, RF, RI>;
+    plan_note(" %dx%d", N1, N2);
     k.poff = k.p.chan0 & 1;
     k.npairs = (k.p.nchan + k.poff + 1) / 2;
     char *w = reinterpret_cast<char *>(k.p.work);
@@ -2605,6 +2612,7 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     if constexpr (PC::kRegCols) {
         if (fold_source(k.p)) {
             k_pairA_fold<PC, T><<<gc, dim3(T), 0, st>>>(k);
+            plan_note(" A:fold");
             launched = true;
         }
     }
@@ -2613,11 +2621,14 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
         if (fast_source(k.p)) {
             if (k.p.prof_rows == 1) k_pairA_fast<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
             else k_pairA_fast<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
+            plan_note(k.p.prof_rows == 1 ? " A:fast_shared" : " A:fast");
         } else {
             k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
+            plan_note(" A:generic");
         }
     } else {
         k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
+        plan_note(" A:generic");
     }
     tk_end(st);
     LAUNCHCHK();
@@ -2633,17 +2644,22 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
         using PRS = PairRowsSeq<N2, TS, RF, RI>;
         k_pair_row_seq<PRS, TS, false><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2 - 1)), dim3(TS), 0, st>>>(k);
         k_pair_row_seq<PRS, TS, true><<<dim3((unsigned)k.npairs, 1u), dim3(TS), 0, st>>>(k);
+        plan_note(" R:pair_row_seq");
     } else if (k.p.htab) {
         k_pair_row<PR, TR, false, true><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
+        plan_note(" R:pair_row_htab");
     } else if (k.p.tail_a) {
         k_pair_row<PR, TR, true><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
+        plan_note(" R:pair_row_tail");
     } else if constexpr (N2 == 8192) {
         constexpr int TS = N2 / 16;                  // 16 values of each row per thread
         using PRS = PairRowsSeq<N2, TS, RF, RI>;
         k_pair_row_seq<PRS, TS, false><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2 - 1)), dim3(TS), 0, st>>>(k);
         k_pair_row_seq<PRS, TS, true><<<dim3((unsigned)k.npairs, 1u), dim3(TS), 0, st>>>(k);
+        plan_note(" R:pair_row_seq");
     } else {
         k_pair_row<PR, TR><<<dim3((unsigned)k.npairs, (unsigned)(N1 / 2)), dim3(TR), 0, st>>>(k);
+        plan_note(" R:pair_row");
     }
     tk_end(st);
     LAUNCHCHK();
@@ -2653,11 +2669,14 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     tk_begin(TK_COLC, st);
     if (fast) {
         if constexpr (PCC::kItemsExact) {
-            if constexpr (N1 == 2048 && N2 % 16 == 0)
+            if constexpr (N1 == 2048 && N2 % 16 == 0) {
                 k_pairC_fast32<PairCols<N1, 16, 512, CF, CI, -1>, 512>
                     <<<dim3((unsigned)(N2 / 16), (unsigned)k.npairs), dim3(512), 0, st>>>(k);
-            else
+                plan_note(" C:fast32");
+            } else {
                 k_pairC_fast<PCC, TC><<<dim3((unsigned)(N2 / BC), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
+                plan_note(" C:fast");
+            }
         }
     } else if (PC::kRegCols && fold_epilogue(k)) {
         if constexpr (PC::kRegCols) {
@@ -2666,9 +2685,11 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
             constexpr int FB = B > 128 ? 128 : B;
             using PCF = PairCols<N1, FB, FB, CF, CI>;
             k_pairC_fold<PCF, FB><<<dim3((unsigned)(N2 / FB), (unsigned)k.npairs), dim3(FB), 0, st>>>(k);
+            plan_note(" C:fold");
         }
     } else {
         k_pairC<PC, T><<<gc, dim3(T), 0, st>>>(k);
+        plan_note(" C:generic");
     }
     tk_end(st);
     LAUNCHCHK();
@@ -2676,6 +2697,7 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
         if (k.mask_ready) HIPCHK(hipStreamWaitEvent(st, k.mask_ready, 0));
         const int rc = launch_null_fix(k, st);
         if (rc) return rc;
+        plan_note(" N:fix_list");
     }
     return PSS_OK;
 }

@@ -975,6 +975,7 @@ static int launch_null_refine(KP &k, hipStream_t st) {
     LAUNCHCHK();
     k_null_refine<<<gs, dim3(256), 0, st>>>(k, W1, B, mx, cnt, cap);     // (overflow only)
     LAUNCHCHK();
+    plan_note(cap ? " N:refine_list" : " N:refine_per_sample");
     return PSS_OK;
 }
 
@@ -1004,6 +1005,8 @@ static int run_bluestein(KP &k, hipStream_t st) {
     // reads them), so they may start on 128-B lines where W1 has the room
     const int64_t ldp = (k.N + 15) & ~(int64_t)15;
     if (fused && k.npairs * ldp <= (int64_t)k.p.nchan * k.N) a.ld = ldp;
+    plan_note("bluestein %lldx%lld %s%s", (long long)g.M1, (long long)g.M2, pair ? "pair" : "rows",
+              fused ? " fused" : "");
     tk_begin(TK_FALLBACK, st);
     if (!pair) k_fb_source<<<ge, dim3(256), 0, st>>>(k);
     else if (!fused) k_fb_source_pair<<<ge, dim3(256), 0, st>>>(k);
@@ -1038,6 +1041,7 @@ static int run_bluestein(KP &k, hipStream_t st) {
 int run_fallback(KP &k, hipStream_t st) {
     if (bs_len(k.N) && !(g_flags & PSS_FLAG_DIRECT_DFT)) return run_bluestein(k, st);
     dim3 g = stream_grid((k.N + 3) / 4, k.p.nchan);
+    plan_note("direct");
     tk_begin(TK_FALLBACK, st);
     k_fb_source<<<g, dim3(256), 0, st>>>(k);
     LAUNCHCHK();

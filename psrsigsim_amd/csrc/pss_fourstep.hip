@@ -283,6 +283,7 @@ int launch_null_fix(const KP &k, hipStream_t st) {
 
 int run_fourstep(KP &k, hipStream_t st, const float *mask_row) {
     const int64_t N = k.N;
+    plan_note("fourstep");
     if (N == (1 << 22)) {
         // C3: 1024 x 4096 (two 4096-point rows of a pair in 66 KB: two row
         // workgroups per CU; 16-column pass-C blocks, 64-B output segments)

@@ -69,6 +69,18 @@ void tk_end(hipStream_t st) {
 
 int g_flags = 0;   // pss_set_flags (test hook)
 
+// launch-plan log: one line per pss_run since the last pss_plan_collect
+static char g_plan[16384];
+static size_t g_plan_len = 0;
+void plan_note(const char *fmt, ...) {
+    if (g_plan_len + 1 >= sizeof(g_plan)) return;
+    va_list ap;
+    va_start(ap, fmt);
+    const int w = vsnprintf(g_plan + g_plan_len, sizeof(g_plan) - g_plan_len, fmt, ap);
+    va_end(ap);
+    if (w > 0) g_plan_len = std::min(g_plan_len + (size_t)w, sizeof(g_plan) - 1);
+}
+
 SideStreams *side_streams() {
     static SideStreams g[64];
     int dev = 0;
@@ -129,6 +141,7 @@ __global__ __launch_bounds__(256) void k_elementwise(KP k) {
 
 int launch_elementwise(const KP &k, hipStream_t st) {
     dim3 g = stream_grid((k.N + 3) / 4, k.p.nchan);
+    plan_note(k.mtab ? " elementwise" : "elementwise");
     tk_begin(TK_ELEM, st);
     k_elementwise<<<g, dim3(256), 0, st>>>(k);
     tk_end(st);
@@ -378,6 +391,18 @@ int pss_timing_collect(int32_t *kind, double *ms, int64_t *units, int cap) {
     return n;
 }
 
+int pss_plan_collect(char *buf, size_t n) {
+    const int len = (int)g_plan_len;
+    if (buf && n) {
+        const size_t c = std::min(n - 1, g_plan_len);
+        memcpy(buf, g_plan, c);
+        buf[c] = 0;
+    }
+    g_plan_len = 0;
+    g_plan[0] = 0;
+    return len;
+}
+
 int pss_last_error(char *buf, size_t n) {
     if (buf && n) {
         strncpy(buf, g_err, n - 1);
@@ -396,6 +421,8 @@ static int run_paths(const PssPipeline *p, hipStream_t st);
 int pss_run(const PssPipeline *p, void *stream) {
     int rc = validate(p);
     if (rc) return rc;
+    if (g_plan_len) plan_note("\n");
+    plan_note("%dx%lld: ", p->nchan, (long long)p->nsamp);
     hipStream_t st = (hipStream_t)stream;
     const bool windows = p->out_kind != PSS_OUT_NONE && p->out_len > 0;
     if (windows) HIPCHK(hipMemsetAsync(p->out_acc, 0, (size_t)p->nchan * (size_t)p->out_len * 8, st));

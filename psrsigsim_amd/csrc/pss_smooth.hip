@@ -10,6 +10,7 @@ int run_smooth(KP &k, hipStream_t st) {
     if (!smooth_split(k.N, &n1, &n2)) return fail(PSS_EUNSUPPORTED, "N=%lld", (long long)k.N);
     k.N1 = n1;
     k.N2 = n2;
+    plan_note("smooth");
     switch (n1) {
         case 6:  return launch_smooth_n2<6, RList<2, 3>, RList<3, 2>, 256>(k, st);
         case 10: return launch_smooth_n2<10, RList<2, 5>, RList<5, 2>, 256>(k, st);

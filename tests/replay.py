@@ -283,6 +283,24 @@ def _err(gpu, ref, exclude=None, scale_ref=None):
     return float(np.max(np.max(np.abs(gpu2 - ref2), axis=1) / scale))
 
 
+def assert_plan(lines, nchan, nsamp, tokens, absent=()):
+    """The last pss_run of an nchan x nsamp run in a launch-plan log
+    (psrsigsim_amd._lib.plan_collect) picked every kernel named in
+    ``tokens`` ("fourstep", "1024x4096", "A:fast", "R:pair_row", "C:fast",
+    "N:fix_list", ...) and none in ``absent``: the parity tests name the
+    kernels whose bits they check, so a dispatch change cannot move them
+    onto other kernels unnoticed."""
+    pref = "%dx%d:" % (nchan, nsamp)
+    runs = [l for l in lines if l.startswith(pref)]
+    assert runs, ("no %s run in the plan log" % pref, lines)
+    got = set(runs[-1][len(pref):].split())
+    missing = set(tokens) - got
+    extra = set(absent) & got
+    assert not missing and not extra, ("kernel plan %r: missing %s, unexpected %s" % (runs[-1], sorted(missing),
+                                                                                     sorted(extra)))
+    return runs[-1]
+
+
 def run_case(name, fused=True, case=None, seed=None):
     """Replay a golden case (``name``) -- or, with ``case``/``seed``, any case
     script against the oracle run with legacy RandomState(seed) draws."""

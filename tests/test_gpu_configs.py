@@ -1,9 +1,12 @@
 """GPU parity for the BASELINE configs and reference fixtures not covered by
 the golden replays (VERDICT r01 "next round" item 1):
 
-* C5 -- the 2^24-sample power-of-two four-step (2048 x 8192 split, 8-column
-  fast pass C) at DM 500 with a delayed null, channels of the 8192-channel
-  band, against the oracle with injected draws; full-size properties at 2^24
+* C5 -- the 2^24-sample power-of-two four-step at DM 500 (with a delayed
+  null: the 2048 x 8192 split and its mask table; without: 1024 x 16384 and
+  the 16384-point row pass), channels of the 8192-channel band, against the
+  oracle with injected draws (so the generic column passes: the fast ones
+  draw their own Philox values, tests/test_gpu_fastpath_oracle.py); the
+  split each run takes is asserted (pss_plan_collect); full-size properties at 2^24
   (integer shift == np.roll; the fast/generic bitwise check is in
   test_gpu_stats.py);
 * C2 -- NANOGrav search mode, 2^20 samples, J1713+0747 DataProfile, GBT
@@ -48,7 +51,11 @@ def test_c5_2p24_fourstep_vs_oracle(chans, null, hip_lib):
     """Global channels of C5's 8192-channel band (lowest band edge: the
     largest delay, ~7e4 samples; an odd-sized shard off the pair parity),
     staged and fused are the same kernels at this size: fused only."""
+    from psrsigsim_amd import _lib
+    _lib.plan_collect()
     _ok(replay.run_case(None, fused=True, case=_c5_case(chans, null), seed=24 + chans[0]))
+    plan = ("2048x8192", "R:pair_row_seq", "N:table") if null else ("1024x16384", "R:pair_row_seq")
+    replay.assert_plan(_lib.plan_collect(), chans[1] - chans[0], 1 << 24, ("fourstep",) + plan)
 
 
 def test_c5_integer_shift_is_roll(hip_lib):

@@ -8,7 +8,9 @@ own Philox draws, not injected ones.  And the C5 geometry (VERDICT r04 item
 noise -- without a null (BASELINE C5: the 1024 x 16384 split, C3's
 k_pairA_fast / k_pairC_fast and the 16384-point k_pair_row_seq) and with a
 delayed null(0.1) (the 2048 x 8192 split: k_pairA_fast on 2048-point
-columns, the 8192-point k_pair_row_seq, k_pairC_fast32, k_null_fix_list).  The draws are then recovered with
+columns, the 8192-point k_pair_row_seq, k_pairC_fast32, k_null_fix_list).
+Each run asserts through the launch-plan log (pss_plan_collect) that these
+kernels, and no generic pass, produced the bits it checks.  The draws are then recovered with
 pss_chi2_fill (the same counter-based keys: seed, call id, purpose, global
 channel, sample) and replayed through the CPU oracle in the reference's
 draw order (pulses, null pulse choice, box values, replacements, noise).
@@ -73,12 +75,17 @@ class _PhiloxReplay(object):
 # (name, log2 N, band channels, scatter_broaden(convolve), DM, null)
 GEOMS = {"c3": (22, 2048, True, 100, True), "c5": (24, 8192, False, 500, False),
          "c5_null": (24, 8192, False, 500, True)}
+# the kernels each geometry must run (pss_plan_collect tokens)
+PLANS = {"c3": ("fourstep", "1024x4096", "A:fast", "R:pair_row", "C:fast", "N:table", "N:fix_list"),
+         "c5": ("fourstep", "1024x16384", "A:fast_shared", "R:pair_row_seq", "C:fast"),
+         "c5_null": ("fourstep", "2048x8192", "A:fast_shared", "R:pair_row_seq", "C:fast32", "N:table",
+                     "N:fix_list")}
 
 
 @pytest.mark.parametrize("geom", sorted(GEOMS))
 def test_fast_path_channels_vs_oracle(geom, hip_lib):
     import psrsigsim_amd as pss
-    from psrsigsim_amd import _engine
+    from psrsigsim_amd import _engine, _lib
     from psrsigsim_amd.signal import FilterBankSignal
     from psrsigsim_amd.pulsar import Pulsar, GaussProfile
     from psrsigsim_amd.ism import ISM
@@ -95,8 +102,10 @@ def test_fast_path_channels_vs_oracle(geom, hip_lib):
     ism.disperse(sig, dm)
     if null:
         psr.null(sig, 0.1)                                  # call 2
+    _lib.plan_collect()
     T.Arecibo().observe(sig, psr, system="Lband_PUPPI", noise=True)   # call 3 / 2 (no copy: fast epilogue)
     got = sig.data.cpu().numpy().astype(np.float64)
+    replay.assert_plan(_lib.plan_collect(), C, N, PLANS[geom], absent=("A:generic", "C:generic"))
     # the device's draws, recovered by key
     gen = _fill(C, 0, N, 1.0, seed, 1, P_PULSE)
     if null:
