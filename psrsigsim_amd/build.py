@@ -27,13 +27,19 @@ OUT_DEBUG = os.path.join(HERE, "libpss_hip_debug.so")
 ARCH = os.environ.get("PSS_OFFLOAD_ARCH", "gfx950")
 # -fno-slp-vectorize: packed f32 (v_pk_*) issues at half rate on gfx950 and
 # costs register-pair moves; scalar f32 is cheaper here.
+# -target-feature -packed-fp32-ops (device): without it the backend still
+# forms v_pk_add_f32 from complex adds of 64-bit loaded pairs (34 in pass A,
+# 50 in the row pass); measured 7.65 cycles per wave-instruction at 4 waves
+# per SIMD against 2.54 for v_add_f32 (tools/probe_rates.hip,
+# profiles/r06/probe_rates.txt): row pass -0.23 ms at C3 (same-box A/B,
+# profiles/r06/ab_pk.txt).  The host compile ignores the feature (a warning).
 # -ffp-contract=on: a multiply-add fuses only within one source expression,
 # never across statements, so a value's rounding does not depend on the code
 # around it (HIP's default fuses e.g. the wave pass A's profile x draw
 # product into the first butterfly, which the LDS-staged kernels cannot: the
 # fast and generic kernels would differ by an ulp; ~1 % of pass A's VALU).
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-fno-slp-vectorize",
-         "-ffp-contract=on"]
+         "-ffp-contract=on", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 
 
 def source_hash(extra=()):

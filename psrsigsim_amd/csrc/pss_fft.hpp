@@ -93,49 +93,7 @@ __device__ __forceinline__ void dft5(cf *a) {
     a[3] = csub(r2, i2);
 }
 
-// In-register DFT of size R: 3 and 5 directly; powers of two by recursive
-// radix-2 DIT (with full unrolling every index and twiddle is a compile-time
-// constant).
-template <int R, bool INV>
-__device__ __forceinline__ void dft(cf *a) {
-    if constexpr (R == 3) {
-        dft3<INV>(a);
-    } else if constexpr (R == 5) {
-        dft5<INV>(a);
-    } else if constexpr (R == 2) {
-        cf t = a[1];
-        a[1] = csub(a[0], t);
-        a[0] = cadd(a[0], t);
-    } else if constexpr (R > 2) {
-        constexpr int H = R / 2;
-        cf e[H], o[H];
-#pragma unroll
-        for (int i = 0; i < H; ++i) {
-            e[i] = a[2 * i];
-            o[i] = a[2 * i + 1];
-        }
-        dft<H, INV>(e);
-        dft<H, INV>(o);
-#pragma unroll
-        for (int k = 0; k < H; ++k) {
-            cf t = rot<R, INV>(k, o[k]);
-            a[k] = cadd(e[k], t);
-            a[k + H] = csub(e[k], t);
-        }
-    }
-}
-
-// --------------------------------------------------------------------------
-// Register-resident DFT of a short mixed-radix length (the fold-mode
-// four-step's columns, N1 in {6, 10, 12, 20, 24, 30, 40, 48, 60}): one thread
-// holds a whole column, so the transform needs no LDS exchange at all.
-// Decimation in time, N = R M (R = 4, 2, 3 or 5): the R decimated
-// subsequences x[R m + r] are transformed recursively, then for every k < M
-// the radix-R butterfly over r of W_N^{r k} Y_r[k] gives X[k + M q].  With
-// full unrolling every twiddle is a compile-time constant (cx_cospi below:
-// double-precision Taylor series evaluated by the compiler, rounded once to
-// fp32; exact 0 / +-1 at multiples of pi/2).
-// --------------------------------------------------------------------------
+// Compile-time cos / sin (double-precision series evaluated by the compiler).
 constexpr double cx_pi = 3.14159265358979323846;
 // cos(pi x) for x in [-1, 1] by range reduction to [-1/4, 1/4] and Taylor series
 constexpr double cx_cospi_red(double x, bool sin_form) {
@@ -161,6 +119,92 @@ constexpr double cx_cospi(double x) {
     return -cx_cospi_red(1.0 - x, false);
 }
 constexpr double cx_sinpi(double x) { return cx_cospi(x - 0.5); }
+
+// The radix-2 DIT butterfly with a compile-time twiddle w = e^{-+2 pi i K/R}
+// (forward: minus): p = e + w o, m = e - w o in six fused multiply-adds
+// instead of a complex product and two complex adds (eight): o w = c u with
+// u = (o.x - (s/c) o.y, o.y + (s/c) o.x) when |c| >= |s| (else s u', u' =
+// ((c/s) o.x - o.y, (c/s) o.y + o.x)), so the ratio folds into u and the
+// scale into the adds (Linzer & Feig's FMA butterfly); w = +-1, +-i need no
+// product.
+template <int R, int K, bool INV>
+__device__ __forceinline__ void bfly(cf e, cf o, cf &p, cf &m) {
+    constexpr int k = ((K % R) + R) % R;
+    if constexpr (k == 0) {
+        p = cadd(e, o);
+        m = csub(e, o);
+    } else if constexpr (4 * k == R) {
+        const cf t = INV ? make_float2(-o.y, o.x) : make_float2(o.y, -o.x);
+        p = cadd(e, t);
+        m = csub(e, t);
+    } else {
+        constexpr double cd = cx_cospi(2.0 * k / R);
+        constexpr double sd = (INV ? 1.0 : -1.0) * cx_sinpi(2.0 * k / R);
+        constexpr bool by_c = (cd < 0 ? -cd : cd) >= (sd < 0 ? -sd : sd);
+        constexpr float sc = (float)(by_c ? cd : sd);              // the scale: c or s
+        constexpr float r = (float)(by_c ? sd / cd : cd / sd);      // tan or cot
+        cf u;
+        if constexpr (by_c) {
+            if constexpr (r == 1.0f) {
+                u = make_float2(o.x - o.y, o.y + o.x);
+            } else if constexpr (r == -1.0f) {
+                u = make_float2(o.x + o.y, o.y - o.x);
+            } else {
+                u = make_float2(fmaf(-r, o.y, o.x), fmaf(r, o.x, o.y));
+            }
+        } else {
+            u = make_float2(fmaf(r, o.x, -o.y), fmaf(r, o.y, o.x));
+        }
+        p = make_float2(fmaf(sc, u.x, e.x), fmaf(sc, u.y, e.y));
+        m = make_float2(fmaf(-sc, u.x, e.x), fmaf(-sc, u.y, e.y));
+    }
+}
+template <int R, int K, int H, bool INV>
+__device__ __forceinline__ void bfly_all(const cf *e, const cf *o, cf *a) {
+    if constexpr (K < H) {
+        bfly<R, K, INV>(e[K], o[K], a[K], a[K + H]);
+        bfly_all<R, K + 1, H, INV>(e, o, a);
+    }
+}
+
+// In-register DFT of size R: 3 and 5 directly; powers of two by recursive
+// radix-2 DIT (with full unrolling every index and twiddle is a compile-time
+// constant).
+template <int R, bool INV>
+__device__ __forceinline__ void dft(cf *a) {
+    if constexpr (R == 3) {
+        dft3<INV>(a);
+    } else if constexpr (R == 5) {
+        dft5<INV>(a);
+    } else if constexpr (R == 2) {
+        cf t = a[1];
+        a[1] = csub(a[0], t);
+        a[0] = cadd(a[0], t);
+    } else if constexpr (R > 2) {
+        constexpr int H = R / 2;
+        cf e[H], o[H];
+#pragma unroll
+        for (int i = 0; i < H; ++i) {
+            e[i] = a[2 * i];
+            o[i] = a[2 * i + 1];
+        }
+        dft<H, INV>(e);
+        dft<H, INV>(o);
+        bfly_all<R, 0, H, INV>(e, o, a);
+    }
+}
+
+// --------------------------------------------------------------------------
+// Register-resident DFT of a short mixed-radix length (the fold-mode
+// four-step's columns, N1 in {6, 10, 12, 20, 24, 30, 40, 48, 60}): one thread
+// holds a whole column, so the transform needs no LDS exchange at all.
+// Decimation in time, N = R M (R = 4, 2, 3 or 5): the R decimated
+// subsequences x[R m + r] are transformed recursively, then for every k < M
+// the radix-R butterfly over r of W_N^{r k} Y_r[k] gives X[k + M q].  With
+// full unrolling every twiddle is a compile-time constant (cx_cospi above:
+// double-precision Taylor series evaluated by the compiler, rounded once to
+// fp32; exact 0 / +-1 at multiples of pi/2).
+// --------------------------------------------------------------------------
 
 // W_N^k x = e^{-+2 pi i k / N} x with a compile-time k (forward: minus)
 template <int N, int K, bool INV>
