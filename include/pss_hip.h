@@ -301,6 +301,9 @@ int pss_fold_periods(const float *data, float *out, int32_t nchan, int64_t ld, i
  *                          (interval = last x_i <= phase, end pieces extrapolate)
  *   pss_host_device_table: out[rows][nint][4] (float32) = c * (h^3, h^2, h, 1)
  *                          / amax (the table the source stage evaluates)
+ *   pss_host_pchip_eval:   pchip_coef then ppoly_eval (then / div when div != 1)
+ *                          fused per row: no coefficient table in memory
+ *   pss_host_pchip_table:  pchip_coef then device_table fused per row (hcell = h)
  */
 int pss_host_pchip_coef(const double *x, int64_t K, const double *y, int64_t rows, double *c,
                         int nthreads);
@@ -308,6 +311,10 @@ int pss_host_ppoly_eval(const double *x, int64_t K, const double *c, int64_t row
                         int64_t n, double *out, int nthreads);
 int pss_host_device_table(const double *c, int64_t rows, int64_t nint, double h, double amax,
                           float *out, int nthreads);
+int pss_host_pchip_eval(const double *x, int64_t K, const double *y, int64_t rows, const double *ph, int64_t n,
+                        double div, double *out, int nthreads);
+int pss_host_pchip_table(const double *x, int64_t K, const double *y, int64_t rows, double hcell, double amax,
+                         float *out, int nthreads);
 
 /* Pulsar.null's shift_val (pulsar/pulsar.py:285-288) on the device:
  *   shift_val = count / 2 - argmax(row[0:count])

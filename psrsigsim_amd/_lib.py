@@ -74,6 +74,10 @@ EXPORTS = {
     "pss_chi2_fill": (ctypes.c_int, [c_vp, c_i32, c_i32, c_i64, c_f32, c_u64, c_u32, c_u32, c_vp]),
     "pss_host_pchip_coef": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, ctypes.c_int]),
     "pss_host_ppoly_eval": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, ctypes.c_int]),
+    "pss_host_pchip_eval": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, ctypes.c_double, c_vp,
+                                           ctypes.c_int]),
+    "pss_host_pchip_table": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, ctypes.c_double, ctypes.c_double, c_vp,
+                                            ctypes.c_int]),
     "pss_host_device_table": (ctypes.c_int, [c_vp, c_i64, c_i64, ctypes.c_double, ctypes.c_double,
                                              c_vp, ctypes.c_int]),
 }
@@ -237,6 +241,29 @@ def host_ppoly_eval(x, c, ph):
     out = np.empty((c.shape[0], ph.size))
     check(load().pss_host_ppoly_eval(_dptr(x), x.size, _dptr(c), c.shape[0], _dptr(ph), ph.size,
                                      _dptr(out), host_threads()), "pss_host_ppoly_eval")
+    return out
+
+
+def host_pchip_eval(x, y, ph, div=1.0):
+    """pchip_coefficients then ppoly_eval (then / div), fused per row."""
+    import numpy as np
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    ph = np.ascontiguousarray(ph, dtype=np.float64).ravel()
+    out = np.empty((y.shape[0], ph.size))
+    check(load().pss_host_pchip_eval(_dptr(x), x.size, _dptr(y), y.shape[0], _dptr(ph), ph.size, float(div),
+                                     _dptr(out), host_threads()), "pss_host_pchip_eval")
+    return out
+
+
+def host_pchip_table(x, y, h, amax):
+    """pchip_coefficients then host_device_table, fused per row."""
+    import numpy as np
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    out = np.empty((y.shape[0], x.size - 1, 4), dtype=np.float32)
+    check(load().pss_host_pchip_table(_dptr(x), x.size, _dptr(y), y.shape[0], float(h), float(amax),
+                                      _dptr(out), host_threads()), "pss_host_pchip_table")
     return out
 
 

@@ -61,6 +61,64 @@ void parallel_rows(int64_t rows, int nthreads, F fn) {
 
 extern "C" {
 
+}  // extern "C"
+
+namespace {
+
+// One row's PCHIP coefficients (the NumPy statement's operations, in order):
+// m, d (slopes) are scratch of K - 1 and K; cr receives (K - 1) x 4.
+inline void pchip_row(const double *h, int64_t K, const double *yr, double *m, double *d, double *cr) {
+    for (int64_t i = 0; i + 1 < K; ++i) m[i] = (yr[i + 1] - yr[i]) / h[i];
+    if (K == 2) {
+        d[0] = d[1] = m[0];
+    } else {
+        for (int64_t i = 1; i + 1 < K; ++i) {
+            const double m0 = m[i - 1], m1 = m[i];
+            const double w1 = 2.0 * h[i] + h[i - 1];
+            const double w2 = h[i] + 2.0 * h[i - 1];
+            const bool flat = (std::signbit(m0) != std::signbit(m1)) || (m1 == 0.0) || (m0 == 0.0);
+            d[i] = flat ? 0.0 : 1.0 / ((w1 / m0 + w2 / m1) / (w1 + w2));
+        }
+        d[0] = edge_slope(h[0], h[1], m[0], m[1]);
+        d[K - 1] = edge_slope(h[K - 2], h[K - 3], m[K - 2], m[K - 3]);
+    }
+    for (int64_t i = 0; i + 1 < K; ++i) {
+        const double d0 = d[i], d1 = d[i + 1], hi = h[i], mi = m[i];
+        const double t = (d0 + d1 - 2.0 * mi) / hi;
+        cr[4 * i + 0] = t / hi;
+        cr[4 * i + 1] = (mi - d0) / hi - t;
+        cr[4 * i + 2] = d0;
+        cr[4 * i + 3] = yr[i];
+    }
+}
+
+// interval = last breakpoint <= phase (searchsorted 'right' - 1), clipped to
+// the end pieces; s = phase - x[i]
+inline void locate(const double *x, int64_t K, const double *ph, int64_t n, int64_t *iv, double *s) {
+    for (int64_t j = 0; j < n; ++j) {
+        int64_t i = (int64_t)(std::upper_bound(x, x + K, ph[j]) - x) - 1;
+        i = std::min<int64_t>(std::max<int64_t>(i, 0), K - 2);
+        iv[j] = i;
+        s[j] = ph[j] - x[i];
+    }
+}
+
+// scipy's PPoly power accumulation (lowest power first)
+inline double ppoly_at(const double *ci, double sj) {
+    double res = ci[3] * 1.0;
+    double z = sj;
+    res = res + ci[2] * z;
+    z = z * sj;
+    res = res + ci[1] * z;
+    z = z * sj;
+    res = res + ci[0] * z;
+    return res;
+}
+
+}  // namespace
+
+extern "C" {
+
 int pss_host_pchip_coef(const double *x, int64_t K, const double *y, int64_t rows, double *c,
                         int nthreads) {
     if (K < 2 || rows < 0 || !x || !y || !c) return PSS_EINVAL;
@@ -68,30 +126,56 @@ int pss_host_pchip_coef(const double *x, int64_t K, const double *y, int64_t row
     for (int64_t i = 0; i + 1 < K; ++i) h[i] = x[i + 1] - x[i];
     parallel_rows(rows, nthreads, [&](int64_t r0, int64_t r1) {
         std::vector<double> m(K - 1), d(K);
+        for (int64_t r = r0; r < r1; ++r) pchip_row(h.data(), K, y + r * K, m.data(), d.data(), c + r * (K - 1) * 4);
+    });
+    return PSS_OK;
+}
+
+// The PCHIP through rows of y at knots x evaluated at phases ph, divided by
+// `div` when div != 1 -- pss_host_pchip_coef then pss_host_ppoly_eval then
+// the division, fused per row (no [rows, K - 1, 4] coefficient table in
+// memory): the same operations, so the same bits.
+int pss_host_pchip_eval(const double *x, int64_t K, const double *y, int64_t rows, const double *ph, int64_t n,
+                        double div, double *out, int nthreads) {
+    if (K < 2 || rows < 0 || n < 0 || !x || !y || !ph || !out) return PSS_EINVAL;
+    std::vector<double> h(K - 1);
+    for (int64_t i = 0; i + 1 < K; ++i) h[i] = x[i + 1] - x[i];
+    std::vector<int64_t> iv(n);
+    std::vector<double> s(n);
+    locate(x, K, ph, n, iv.data(), s.data());
+    const bool dv = div != 1.0;
+    parallel_rows(rows, nthreads, [&](int64_t r0, int64_t r1) {
+        std::vector<double> m(K - 1), d(K), cr((K - 1) * 4);
         for (int64_t r = r0; r < r1; ++r) {
-            const double *yr = y + r * K;
-            for (int64_t i = 0; i + 1 < K; ++i) m[i] = (yr[i + 1] - yr[i]) / h[i];
-            if (K == 2) {
-                d[0] = d[1] = m[0];
-            } else {
-                for (int64_t i = 1; i + 1 < K; ++i) {
-                    const double m0 = m[i - 1], m1 = m[i];
-                    const double w1 = 2.0 * h[i] + h[i - 1];
-                    const double w2 = h[i] + 2.0 * h[i - 1];
-                    const bool flat = (std::signbit(m0) != std::signbit(m1)) || (m1 == 0.0) || (m0 == 0.0);
-                    d[i] = flat ? 0.0 : 1.0 / ((w1 / m0 + w2 / m1) / (w1 + w2));
-                }
-                d[0] = edge_slope(h[0], h[1], m[0], m[1]);
-                d[K - 1] = edge_slope(h[K - 2], h[K - 3], m[K - 2], m[K - 3]);
+            pchip_row(h.data(), K, y + r * K, m.data(), d.data(), cr.data());
+            double *o = out + r * n;
+            for (int64_t j = 0; j < n; ++j) {
+                const double v = ppoly_at(cr.data() + 4 * iv[j], s[j]);
+                o[j] = dv ? v / div : v;
             }
-            double *cr = c + r * (K - 1) * 4;
-            for (int64_t i = 0; i + 1 < K; ++i) {
-                const double d0 = d[i], d1 = d[i + 1], hi = h[i], mi = m[i];
-                const double t = (d0 + d1 - 2.0 * mi) / hi;
-                cr[4 * i + 0] = t / hi;
-                cr[4 * i + 1] = (mi - d0) / hi - t;
-                cr[4 * i + 2] = d0;
-                cr[4 * i + 3] = yr[i];
+        }
+    });
+    return PSS_OK;
+}
+
+// DataPortrait.device_table straight from the knot values: pss_host_pchip_coef
+// then pss_host_device_table, fused per row (the same operations and bits).
+int pss_host_pchip_table(const double *x, int64_t K, const double *y, int64_t rows, double hcell, double amax,
+                         float *out, int nthreads) {
+    if (K < 2 || rows < 0 || !x || !y || !out) return PSS_EINVAL;
+    std::vector<double> h(K - 1);
+    for (int64_t i = 0; i + 1 < K; ++i) h[i] = x[i + 1] - x[i];
+    const double w[4] = {pow(hcell, 3.0), pow(hcell, 2.0), hcell, 1.0};
+    const bool dv = amax != 1.0;
+    parallel_rows(rows, nthreads, [&](int64_t r0, int64_t r1) {
+        std::vector<double> m(K - 1), d(K), cr((K - 1) * 4);
+        for (int64_t r = r0; r < r1; ++r) {
+            pchip_row(h.data(), K, y + r * K, m.data(), d.data(), cr.data());
+            float *o = out + r * (K - 1) * 4;
+            for (int64_t e = 0; e < (K - 1) * 4; ++e) {
+                double v = cr[e] * w[e & 3];
+                if (dv) v = v / amax;
+                o[e] = (float)v;
             }
         }
     });
@@ -101,32 +185,14 @@ int pss_host_pchip_coef(const double *x, int64_t K, const double *y, int64_t row
 int pss_host_ppoly_eval(const double *x, int64_t K, const double *c, int64_t rows, const double *ph,
                         int64_t n, double *out, int nthreads) {
     if (K < 2 || rows < 0 || n < 0 || !x || !c || !ph || !out) return PSS_EINVAL;
-    // interval = last breakpoint <= phase (searchsorted 'right' - 1), clipped
-    // to the end pieces; s = phase - x[i]
     std::vector<int64_t> iv(n);
     std::vector<double> s(n);
-    for (int64_t j = 0; j < n; ++j) {
-        int64_t i = (int64_t)(std::upper_bound(x, x + K, ph[j]) - x) - 1;
-        i = std::min<int64_t>(std::max<int64_t>(i, 0), K - 2);
-        iv[j] = i;
-        s[j] = ph[j] - x[i];
-    }
+    locate(x, K, ph, n, iv.data(), s.data());
     parallel_rows(rows, nthreads, [&](int64_t r0, int64_t r1) {
         for (int64_t r = r0; r < r1; ++r) {
             const double *cr = c + r * (K - 1) * 4;
             double *o = out + r * n;
-            for (int64_t j = 0; j < n; ++j) {
-                const double *ci = cr + 4 * iv[j];
-                const double sj = s[j];
-                double res = ci[3] * 1.0;
-                double z = sj;
-                res = res + ci[2] * z;
-                z = z * sj;
-                res = res + ci[1] * z;
-                z = z * sj;
-                res = res + ci[0] * z;
-                o[j] = res;
-            }
+            for (int64_t j = 0; j < n; ++j) o[j] = ppoly_at(cr + 4 * iv[j], s[j]);
         }
     });
     return PSS_OK;

@@ -347,13 +347,28 @@ class DataPortrait(PulsePortrait):
             self._coef_cache = pchip_coefficients(self._knots, self._kvals)
         return self._coef_cache
 
+    def _knot_hit(self, ph):
+        return ph.size <= self._knots.size and np.array_equal(ph, self._knots[:ph.size])
+
     def _generator(self, phases):
         ph = np.asarray(phases, dtype=float)
-        if ph.size <= self._knots.size and np.array_equal(ph, self._knots[:ph.size]):
+        if self._knot_hit(ph):
             return like_rows(np.array(rows_of(self._kvals)[:, :ph.size]), self._kvals)
+        if self._coef_cache is None:
+            # no coefficient table needed: PCHIP built and evaluated per row
+            return like_rows(_lib.host_pchip_eval(self._knots, rows_of(self._kvals), ph), self._kvals)
         return ppoly_eval(self._knots, self._coef, phases, self._kvals)
 
     def calc_profiles(self, phases, Nchan=None):
+        ph = np.asarray(phases, dtype=float)
+        if hasattr(self, '_Amax'):
+            # the division by Amax fused into the one pass that makes the rows
+            # (the same IEEE operations as generator-then-divide)
+            if self._knot_hit(ph):
+                return like_rows(rows_of(self._kvals)[:, :ph.size] / self.Amax, self._kvals)
+            if self._coef_cache is None:
+                return like_rows(_lib.host_pchip_eval(self._knots, rows_of(self._kvals), ph, self.Amax),
+                                 self._kvals)
         profiles = self._generator(phases)
         Amax = self.Amax if hasattr(self, '_Amax') else _band_max(profiles, self._rowset)
         return like_rows(rows_of(profiles) / Amax, profiles)
@@ -386,7 +401,10 @@ class DataPortrait(PulsePortrait):
         h = 1.0 / M
         amax = self.Amax if hasattr(self, '_Amax') else 1.0
         # = (self._coef * [h**3, h**2, h, 1] / amax).astype(float32), natively
-        # (one row for a uniform table: the device then shares it)
+        # (one row for a uniform table: the device then shares it); straight
+        # from the knot values when no coefficient table exists yet
+        if self._coef_cache is None:
+            return _lib.host_pchip_table(self._knots, rows_of(self._kvals), h, amax), M, nint
         return _lib.host_device_table(np.ascontiguousarray(rows_of(self._coef)), h, amax), M, nint
 
 

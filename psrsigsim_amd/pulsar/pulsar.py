@@ -296,6 +296,7 @@ def _dedupe(tab):
     """One shared row when every channel's table is identical."""
     if is_uniform(tab):
         return np.ascontiguousarray(tab[0:1])
-    if tab.shape[0] > 1 and np.all(tab == tab[0:1]):
+    # (row 1 against row 0 first: per-channel tables differ there already)
+    if tab.shape[0] > 1 and np.array_equal(tab[1], tab[0]) and np.all(tab == tab[0:1]):
         return np.ascontiguousarray(tab[0:1])
     return np.ascontiguousarray(tab)
