@@ -13,7 +13,7 @@ from ..utils.constants import DM_K_VALUE, KOLMOGOROV_BETA
 from ..utils.utils import make_quant
 from .._units import Quantity, to_value
 from .. import _lib
-from ..pulsar.portraits import DataPortrait
+from ..pulsar.portraits import DataPortrait, is_uniform
 from .. import _engine
 
 __all__ = ["ISM"]
@@ -151,7 +151,8 @@ class ISM(object):
             pulsar._Profiles = DataPortrait(self._convolve_rows(
                 full_profs, lambda a, b: np.exp(-(t[None, :] * 1e3) / taur[a:b, None]), Nph), rowset=rs)
             return
-        full_profs = np.array(full_profs)      # convolved per channel (a uniform table no longer is)
+        # (a uniform table -- one profile tiled over the channels -- stays one
+        # row through the convolution's profile side: _convolve_rows)
 
         def tails(a, b):
             # rows [a, b) of the exponential tails, t [s] / tau [ms]; rows past
@@ -180,21 +181,37 @@ class ISM(object):
         threads too (bit for bit the same values)."""
         prof = np.asarray(profiles, dtype=float)
         rows = prof.shape[0] if rows is None else rows
+        uni = is_uniform(prof)
+        if uni:
+            # one profile for every channel (a tiled GaussProfile, C3): its
+            # sum, normalisation and spectrum are computed once -- fftconvolve
+            # broadcasts a 1-row operand over the rows, and every row's
+            # arithmetic is the per-row arithmetic of the full table (the same
+            # bits; tests/test_host_plan.py)
+            prof = prof[:1]
+            ps1 = np.sum(prof, axis=1, keepdims=True)
+            pn1 = np.where(ps1 != 0.0, prof / np.where(ps1 != 0.0, ps1, 1.0), prof)
+            out = np.empty((rows, width))
+        else:
+            out = profiles
 
         def block(a, b):
             kb = kern_rows(a, b)
-            ps = np.sum(prof[a:b], axis=1, keepdims=True)
-            pn = np.where(ps != 0.0, prof[a:b] / np.where(ps != 0.0, ps, 1.0), prof[a:b])
+            if uni:
+                ps, pn = ps1, pn1
+            else:
+                ps = np.sum(prof[a:b], axis=1, keepdims=True)
+                pn = np.where(ps != 0.0, prof[a:b] / np.where(ps != 0.0, ps, 1.0), prof[a:b])
             ks = np.sum(kb, axis=1, keepdims=True)
             kn = np.where(ks != 0.0, kb / np.where(ks != 0.0, ks, 1.0), kb)
             # scipy's FFT convolution batched over rows: bit-identical to the
             # reference's per-row scipy.signal.convolve(..., method='fft')
             # (the reference later makes exact float decisions on these values)
             conv = _fftconvolve(pn, kn, mode='full', axes=1)
-            profiles[a:b, :] = ps * conv[:, :width]
+            out[a:b, :] = ps * conv[:, :width]
 
         _lib.host_rows(rows, block)
-        return profiles
+        return out
 
     def scale_dnu_d(self, dnu_d, nu_i, nu_f, beta=KOLMOGOROV_BETA):
         """ism.py:300-318."""

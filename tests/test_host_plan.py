@@ -170,7 +170,7 @@ def test_pchip_matches_scipy():
     np.testing.assert_allclose(ppoly_eval(x, c, ph), P(ph), rtol=0, atol=1e-13)
 
 
-@pytest.mark.parametrize("nchan", [1, 2, 3, 8, 64])
+@pytest.mark.parametrize("nchan", [1, 2, 3, 8, 64, 2048])
 def test_scatter_convolution_bitwise_vs_reference_structure(nchan):
     """The batched host convolution equals the reference's per-row
     scipy.signal.convolve(method='fft') (via the oracle) bit for bit, and so
@@ -192,6 +192,43 @@ def test_scatter_convolution_bitwise_vs_reference_structure(nchan):
     # always spans the period (nint == M, extrapolated pieces appended)
     assert psr.Profiles.uniform_knots()[1] == opsr.Profiles.knot_x.size - 1
     assert sig._pending.source.nint == sig._pending.source.M
+
+
+@pytest.mark.parametrize("nchan,nph", [(300, 512), (37, 1000), (129, 244)])
+def test_uniform_profile_convolution_equals_per_row_reference(nchan, nph):
+    """A profile tiled over the channels is convolved as ONE row against every
+    channel's tail (ism._convolve_rows): each row equals the reference's own
+    per-row scipy.signal.convolve(method='fft') (ism.py:243-288) bit for bit
+    at lengths whose batched transform does not (the FFT of a many-row batch
+    rounds differently from a single row's at e.g. 1023 / 1999 points)."""
+    import scipy.signal as spsig
+    from psrsigsim_amd.ism import ISM
+    from psrsigsim_amd.pulsar.portraits import tile_rows
+    p1 = np.exp(-0.5 * ((np.linspace(0.0, 1.0, nph) - 0.5) / 0.05) ** 2)
+    t = np.linspace(0, 0.005, nph)
+    tau = np.linspace(0.05, 3.0, nchan)
+    got = ISM()._convolve_rows(tile_rows(p1, nchan), lambda a, b: np.exp(-(t[None, :] * 1e3) / tau[a:b, None]), nph)
+    for i in range(nchan):
+        k = np.exp(-(t * 1e3) / tau[i])
+        ref = p1.sum() * spsig.convolve(p1 / p1.sum(), k / k.sum(), mode='full', method='fft')[:nph]
+        np.testing.assert_array_equal(got[i], ref)
+
+
+def test_native_fused_pchip_bitwise():
+    """pss_host_pchip_eval / pss_host_pchip_table (fit and evaluation, fit
+    and device table, fused per row) == the unfused passes, bit for bit."""
+    from psrsigsim_amd import _lib
+    for x, y in _pchip_cases():
+        c = _lib.host_pchip_coef(x, y)
+        ph = np.concatenate([np.linspace(-0.1, 1.1, 333), x, [0.5 / 244.0]])
+        for div in (1.0, 0.7316):
+            ref = _lib.host_ppoly_eval(x, c, ph)
+            if div != 1.0:
+                ref = ref / div
+            np.testing.assert_array_equal(_lib.host_pchip_eval(x, y, ph, div), ref)
+        h = 1.0 / max(x.size - 1, 1)
+        for amax in (1.0, 0.7316):
+            np.testing.assert_array_equal(_lib.host_pchip_table(x, y, h, amax), _lib.host_device_table(c, h, amax))
 
 
 # ---------------------------------------------------------------------------
