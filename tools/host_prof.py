@@ -1,5 +1,5 @@
 """Host-side profile (cProfile) of a bench workload step on the GPU box:
-where the non-kernel time of a step goes.  usage: tools/host_prof.py c4|c3"""
+where the non-kernel time of a step goes.  usage: tools/host_prof.py c4|c3|t1|t2"""
 import cProfile
 import pstats
 import sys
@@ -11,7 +11,9 @@ import bench
 
 wl = sys.argv[1] if len(sys.argv) > 1 else "c4"
 step = {"c4": lambda: bench.c4_step(pss, 2048, None, False),
-        "c3": lambda: bench.c3_step(pss, 2048, None, 22)}[wl]
+        "c3": lambda: bench.c3_step(pss, 2048, None, 22),
+        "t1": lambda: bench.tutorial_step(pss, "t1", 128, None),
+        "t2": lambda: bench.tutorial_step(pss, "t2", 64, None)}[wl]
 for _ in range(2):
     s = step()
     s.data
