@@ -92,6 +92,10 @@ struct KP {
     hipEvent_t mask_ready;  // mask table built on a side stream: wait before its first use (or NULL)
     const uint32_t *wlist;  // delayed null: table words with a nulled position (any f)
     const uint32_t *nwlist; // its length (device)
+    // single-workgroup kernel with a float64-refined delayed null: the
+    // inverse transform's (data, mask) pairs go to this [nchan][N] buffer
+    // (the packed paths' W1) instead of through the epilogue
+    cf *w1_out;
 };
 // pair spill row pitch and per-pair stride (complex)
 __host__ __device__ __forceinline__ int64_t rpitch(const KP &k) { return k.N2; }
@@ -825,7 +829,15 @@ struct SinglePass<L, BATCH, T, RList<F...>, RList<I...>> {
                 pre[i] = z.x * k.invN;
                 msk[i] = z.y * k.invN;
             }
-            epilogue4(k, r0 + b, n0, 4, pre, msk, !re_in);
+            if (k.w1_out) {
+                // (data, mask) for the float64 null refine; the epilogue runs
+                // after it (k_fb_epilogue, as on the other packed paths)
+                cf *w = k.w1_out + (int64_t)(r0 + b) * L + n0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[i] = make_float2(pre[i], msk[i]);
+            } else {
+                epilogue4(k, r0 + b, n0, 4, pre, msk, !re_in);
+            }
         }
     }
 };
@@ -2218,6 +2230,8 @@ int run_smooth_c(KP &k, hipStream_t st);                          // pss_smooth_
 int run_fourstep_b(KP &k, hipStream_t st, const float *mask_row); // pss_fourstep_b.hip (N != 2^22)
 int run_single(KP &k, hipStream_t st);                            // pss_single.hip
 int run_fallback(KP &k, hipStream_t st);                          // pss_fallback.hip
+int launch_null_refine(KP &k, hipStream_t st);                    // pss_fallback.hip
+int launch_fb_epilogue(KP &k, hipStream_t st);                    // pss_fallback.hip
 int shift_rows_odd(float *rows, int32_t nrows, int64_t n, int64_t ld, const uint64_t *ramp, void *work,
                    hipStream_t st);                               // pss_fallback.hip
 // the mask-table template's (build_mask_table) non-template kernels, launched
@@ -2369,6 +2383,16 @@ static inline WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
         w.mbits = o; o += al256((int64_t)nchan * (N / 8));   // per-channel null bits
         w.rtab = o;  o += al256(npairs * 2 * 64 * 8);          // row-pass pair ramp factors (RFL <= 64)
         w.wlist = o; o += al256((N / 32) * 4);                 // null fix-up: table words with nulls
+    } else if (!filt && is_pow2(N) && N >= 64 && N <= 8192) {
+        // single-workgroup lengths: W1 [nchan][N] cf and the float64 null
+        // refine's buffers (a delayed null: run_single)
+        o += al256((int64_t)nchan * N * 8);
+        w.rf_tw = o; o += al256(N * 16);
+        w.rf_B = o;  o += al256((N / 2 + 1) * 16);
+        w.rf_mx = o; o += al256((int64_t)nchan * 4);
+        w.rf_part = o; o += al256((int64_t)kBsParts * (N / 2 + 1) * 16);
+        w.rf_list = o; o += al256(refine_cap(nchan, N) * 8);
+        w.rf_cnt = o;  o += 256;
     } else if (filt || !(is_pow2(N) && N >= 64 && N <= 8192)) {
         // fallback: W1, W2, twiddles -- Bluestein needs W1 only (its forward
         // and inverse DFTs are fused through Z), unless the mixed-radix
@@ -2406,6 +2430,14 @@ static inline WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
     o += al256(N * 4);
     w.total = o;
     return w;
+}
+
+// The float64 null decisions of the packed paths (k_null_refine): the
+// direct / Bluestein rows and the single-workgroup kernel's, between the
+// inverse transform (W1 = data + i mask per row) and the epilogue.
+static inline bool refine_null(const KP &k) {
+    return k.p.null_mode == PSS_NULL_DELAYED && (k.N & 1) == 0 && k.N <= kRefineMaxN && !k.p.tail_a &&
+           !k.p.htab && !(g_flags & PSS_FLAG_NULL_F32);
 }
 
 // Fast-path selection (kernels specialised for the north-star configuration;

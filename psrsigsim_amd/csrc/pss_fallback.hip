@@ -932,14 +932,8 @@ static int bs_filter_pair(const KP &k, BsArgs a, int64_t nb, int npairs, hipStre
     return PSS_OK;
 }
 
-// The float64 null decisions of the packed paths (k_null_refine), between
-// the inverse transform (W1 = data + i mask per row) and the epilogue.
-static bool refine_null(const KP &k) {
-    return k.p.null_mode == PSS_NULL_DELAYED && (k.N & 1) == 0 && k.N <= kRefineMaxN && !k.p.tail_a &&
-           !k.p.htab && !(g_flags & PSS_FLAG_NULL_F32);
-}
 
-static int launch_null_refine(KP &k, hipStream_t st) {
+int launch_null_refine(KP &k, hipStream_t st) {
     const WsLayout w = ws_layout(k.p.nchan, k.N, k.p.htab != nullptr);
     char *base = reinterpret_cast<char *>(k.p.work);
     cf *W1 = reinterpret_cast<cf *>(base);
@@ -1034,6 +1028,12 @@ static int run_bluestein(KP &k, hipStream_t st) {
     if (refine_null(k) && (rc = launch_null_refine(k, st))) return rc;
     k_fb_epilogue<<<ge, dim3(256), 0, st>>>(k);
     tk_end(st);
+    LAUNCHCHK();
+    return PSS_OK;
+}
+
+int launch_fb_epilogue(KP &k, hipStream_t st) {
+    k_fb_epilogue<<<stream_grid((k.N + 3) / 4, k.p.nchan), dim3(256), 0, st>>>(k);
     LAUNCHCHK();
     return PSS_OK;
 }

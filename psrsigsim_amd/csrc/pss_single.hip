@@ -3,9 +3,7 @@
 
 using namespace pss;
 
-int run_single(KP &k, hipStream_t st) {
-    k.N1 = 1;
-    k.N2 = k.N;
+static int launch_single_n(KP &k, hipStream_t st) {
     switch (k.N) {
         case 64: return launch_single<64, 64, 256, C64F, C64I>(k, st);
         case 128: return launch_single<128, 32, 256, C128F, C128I>(k, st);
@@ -18,5 +16,20 @@ int run_single(KP &k, hipStream_t st) {
         default: break;
     }
     return fail(PSS_EUNSUPPORTED, "single-pass: N=%lld", (long long)k.N);
+}
+
+int run_single(KP &k, hipStream_t st) {
+    k.N1 = 1;
+    k.N2 = k.N;
+    if (!refine_null(k)) return launch_single_n(k, st);
+    // a delayed null decided in float64: the kernel leaves
+    // (data, mask) per sample in W1, the samples within the fp32 error of the
+    // threshold are re-decided from the box row's float64 spectrum
+    // (launch_null_refine), then the epilogue (null, observe copy, noise, store)
+    k.w1_out = reinterpret_cast<cf *>(k.p.work);
+    int rc = launch_single_n(k, st);
+    if (!rc) rc = launch_null_refine(k, st);
+    if (!rc) rc = launch_fb_epilogue(k, st);
+    return rc;
 }
 

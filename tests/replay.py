@@ -43,8 +43,8 @@ AMBIG_REL_TABLE = 2e-6
 # ~2e-6 relative error on a row of ~1e4 values thresholded at 1, not the
 # packing -- kept packed.)
 # Packed lengths whose decisions the device re-evaluates in float64
-# (`k_null_refine`: even N <= 2^17 on the direct / Bluestein paths, no
-# scattering tail; not the single-workgroup 2^m <= 8192 kernel): what is left
+# (`k_null_refine`: even N <= 2^17 on the direct / Bluestein paths and, since
+# round 6, the single-workgroup 2^m <= 8192 kernel; no scattering tail): what is left
 # is the rounding of the fp32 box values the device starts from, <= 6e-8 x
 # sum_j |box_j K(n - j)| (K the shift's interpolation kernel, L1 norm ~5 at
 # these N): band 5e-7 x the mask scale (+ AMBIG absolute).
@@ -55,19 +55,20 @@ REFINED = True      # False while the device runs with PSS_FLAG_NULL_F32 (tools)
 
 def packed64(n, case):
     """Mirrors the device dispatch (pss_run / refine_null): every even N <=
-    2^17 off the single-workgroup kernel (2^m, 64 <= N <= 8192) and off the
-    mask-table four-step (2^m >= 2^14) is decided in float64 -- N = 2 .. 32
-    included (direct DFT) -- unless a scattering tail rides on the transform."""
+    2^17 off the mask-table four-step (2^m >= 2^14) is decided in float64 --
+    the single-workgroup kernel's 2^m <= 8192 (round 6) and N = 2 .. 32
+    (direct DFT) included -- unless a scattering tail rides on the transform."""
     pow2 = n & (n - 1) == 0
-    return (REFINED and n % 2 == 0 and n <= REFINE_MAX_N and not (pow2 and 64 <= n <= 8192)
+    return (REFINED and n % 2 == 0 and n <= REFINE_MAX_N and not (pow2 and n >= 16384)
             and not any(op[0] == "scatter_tail" for op in case["ops"]))
 
 
 # "packed": the float64-decided packed lengths (C4's fold-mode geometry with a
 # delayed null: band 9.3e-4, no flips, against 1.9 % and up to 1.1e-4 flipped
 # with the fp32 decisions, tools/null_band_r4.py, profiles/r04/null_band.txt);
-# "packed_f32": the packed lengths the device still decides in fp32 (the
-# single-workgroup 2^m <= 8192 kernel, N > 2^17, the scattering tail) -- on
+# "packed_f32": the packed lengths the device still decides in fp32 (N >
+# 2^17 off the four-step, the scattering tail; until round 6 also the
+# single-workgroup 2^m <= 8192 kernel) -- on
 # the search-mode cases that reach them (golden northstar_mini: 8192 samples;
 # Bluestein 100002) the measured band is 3.05e-5 / 3.5e-5 with no flip
 # (profiles/r04/null_band.txt), so the bounds sit ~10x above that (VERDICT r04

@@ -44,7 +44,6 @@ def test_library_built_from_these_sources():
 def test_workspace_sizes():
     L = _lib.load()
     # [spill area, 256-B aligned regions][null mask row: nsamp floats]
-    assert L.pss_workspace_bytes(4, 4096) == 4096 * 4               # single pass: LDS only
     n = 1 << 20
     # pair mode: Yd ((nchan+2)//2 pairs, parity-aligned) + mask-table build (Mspec,
     # 6 node pair spills, 12 node rows, table bits/base, worst-case 16-float records,
@@ -62,6 +61,9 @@ def test_workspace_sizes():
     # candidate list -- 1/8 of the samples + 64 Ki entries of 8 B -- and its count)
     f64 = lambda n, nc: (a(n * 16) + a((n // 2 + 1) * 16) + a(nc * 4) + a(16 * (n // 2 + 1) * 16)
                          + a(min(nc * n, nc * n // 8 + 65536) * 8) + 256)
+    # single-workgroup lengths (round 6): W1 [nchan][N] for the float64 null
+    # refine of a delayed null, its buffers, the mask row
+    assert L.pss_workspace_bytes(4, 4096) == a(4 * 4096 * 8) + f64(4096, 4) + 4096 * 4
     sp = 2 * 2 * 244 * 8 + 244 * 8                                   # fallback W1, W2, twiddles
     assert L.pss_workspace_bytes(2, 244) == a(sp) + f64(244, 2) + 1024   # row: 976 B, aligned
     # Bluestein fallback (N > 8192, 2 x 5003): W1 only (forward and inverse

@@ -18,9 +18,10 @@ def test_packed64_lengths():
     c = _case()
     assert replay.packed64(30720, c)            # C4's fold-mode length (direct path)
     assert replay.packed64(10006, c)            # Bluestein
-    assert not replay.packed64(8192, c)         # single-workgroup kernel: fp32
-    assert not replay.packed64(4096, c)
-    assert not replay.packed64(64, c)           # the smallest single-workgroup length
+    assert replay.packed64(8192, c)             # single-workgroup kernel: float64 since round 6
+    assert replay.packed64(4096, c)
+    assert replay.packed64(64, c)               # the smallest single-workgroup length
+    assert not replay.packed64(16384, c)        # mask-table four-step
     assert replay.packed64(32, c)               # 2^m < 64: direct DFT, refined
     assert replay.packed64(16, c)
     assert not replay.packed64(10007, c)        # odd: shift_t only
