@@ -750,7 +750,7 @@ def main():
         # --json, full-size launches): which kernel dominates there and its
         # fraction, reported next to this run's HIP-event figures (the two
         # rankings can differ box to box)
-        for rnd in ("r05", "r04"):
+        for rnd in ("r06", "r05", "r04"):
             kj = os.path.join(ROOT, "profiles", rnd, "kernel_profile.json")
             if args.workload == "c3" and C == NCHAN and nsamp == (1 << LOG2N) and os.path.exists(kj):
                 kp = json.load(open(kj))
@@ -766,7 +766,7 @@ def main():
                     roof["frac_profile_source"] = "profiles/%s/kernel_profile.json (rocprofv3 kernel trace, " \
                                                   "full-size launches)" % rnd
                 break
-        for rnd in ("r05", "r04", "r03", "r02"):
+        for rnd in ("r06", "r05", "r04", "r03", "r02"):
             tj = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
             if args.workload == "c3" and C == NCHAN and nsamp == (1 << LOG2N) and os.path.exists(tj):
                 t = json.load(open(tj)).get(dom)

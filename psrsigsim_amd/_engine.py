@@ -348,10 +348,25 @@ def build_pipeline(sig, pend, rows, chan0, data, out=None, ws_role="main"):
             p.prof = ctypes.c_void_p(src.dev_table.data_ptr() + i * int(src.table[0].size) * 4)
             p.prof_rows = src.table.shape[0] - i
             p.prof_row0 = int(chan0)
-    for name, arr in P["arrays"].items():
-        t = u64_to_i64_tensor(arr) if name in ("ramp", "mask_ramp") else to_dev(arr)
+    if P["arrays"]:
+        # every per-run array in ONE host->device copy (a pinned staging
+        # buffer, 256-B aligned slots): each separate upload costs ~20-40 us of
+        # host time (pinning, a copy launch), which the short runs of the
+        # reference's own shapes (tutorial 2: 64 x 40 960) feel
+        slots, off = [], 0
+        for name, arr in P["arrays"].items():
+            a = np.ascontiguousarray(np.asarray(arr, dtype=np.uint64).view(np.int64)
+                                     if name in ("ramp", "mask_ramp") else arr)
+            slots.append((name, off, a))
+            off += (a.nbytes + 255) & ~255
+        host = np.zeros(max(off, 256), dtype=np.uint8)
+        for _, o, a in slots:
+            host[o:o + a.nbytes] = a.view(np.uint8).ravel()
+        t = to_dev(host)
         keep.append(t)
-        setattr(p, name, ptr(t))
+        base = t.data_ptr()
+        for name, o, _ in slots:
+            setattr(p, name, ctypes.c_void_p(base + o))
     if P.get("shift"):
         ws = workspace(_lib.load().pss_workspace_bytes(rows, sig._ncols), ws_role)
         p.work = ptr(ws) if ws is not None else None
