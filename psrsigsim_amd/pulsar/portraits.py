@@ -199,7 +199,10 @@ class PulsePortrait(object):
         ph = np.arange(Nphase) / Nphase
         self._profiles = self.calc_profiles(ph, Nchan=Nchan)
         self._Amax = _band_max(self._profiles, self._rowset)
-        self._profiles = like_rows(rows_of(self._profiles) / self.Amax, self._profiles)
+        # (x / 1.0 is x: calc_profiles already divided by the band max, so the
+        # renormalisation is the identity unless a rank's rows differ)
+        if self.Amax != 1.0:
+            self._profiles = like_rows(rows_of(self._profiles) / self.Amax, self._profiles)
         self._max_profile = _first_max_row(self._profiles, self._rowset)
 
     def calc_profiles(self, phases, Nchan=None):
@@ -369,6 +372,11 @@ class DataPortrait(PulsePortrait):
             if self._coef_cache is None:
                 return like_rows(_lib.host_pchip_eval(self._knots, rows_of(self._kvals), ph, self.Amax),
                                  self._kvals)
+        if self._knot_hit(ph):
+            # the knot values themselves: the band max over the view, one
+            # division pass (no copy first)
+            kv = rows_of(self._kvals)[:, :ph.size]
+            return like_rows(kv / _band_max(kv, self._rowset), self._kvals)
         profiles = self._generator(phases)
         Amax = self.Amax if hasattr(self, '_Amax') else _band_max(profiles, self._rowset)
         return like_rows(rows_of(profiles) / Amax, profiles)

@@ -13,7 +13,7 @@ import math
 import numpy as np
 
 from .profiles import GaussProfile, DataPortrait
-from .portraits import GaussPortrait, is_uniform
+from .portraits import GaussPortrait, is_uniform, rows_of
 from .._units import make_quant, Quantity, to_value
 from .. import _engine
 
@@ -90,9 +90,14 @@ class Pulsar(object):
                     C = C[rs.gids]
                 else:
                     rs = None
-            if is_uniform(full_profs):
-                full_profs = np.array(full_profs)
-            full_profs *= C   # in place: a 1-row portrait with Nchan > 1 raises, as there
+            if is_uniform(full_profs) and C.shape[0] == full_profs.shape[0]:
+                # the tiled row times C in one pass (the values of the
+                # reference's copy-then-scale-in-place: x * C either way)
+                full_profs = rows_of(full_profs) * C
+            else:
+                if is_uniform(full_profs):
+                    full_profs = np.array(full_profs)
+                full_profs *= C   # in place: a 1-row portrait with Nchan > 1 raises, as there
         self._Profiles = DataPortrait(full_profs, rowset=rs)
 
     def make_pulses(self, signal, tobs):
