@@ -2111,133 +2111,6 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         }
     }
 
-    // C, fast path as a PERSISTENT kernel (one workgroup per CU): with one
-    // 141-KB workgroup per CU every CU runs the same phases at the same time
-    // -- spill loads, column FFTs, output stores -- so HBM alternates between
-    // saturated and idle.  Here each workgroup takes column blocks from its
-    // XCD's counter (ctr[x], blocks [x T/8, (x+1) T/8) in order: the CUs of an
-    // XCD work on neighbouring blocks together, so their 64-B output segments
-    // still meet in the XCD's L2) and loads block i+1's spill into registers
-    // while it transforms and stores block i.  Bitwise passC_fast's values
-    // (the same twiddles, FFT and epilogue per block).
-    __device__ static void passC_fast_persist(const KP &k, unsigned int *ctr) {
-        static_assert(kItemsExact && kWaveCols && B == 16 && ITEMS * T * 4 == N1 * B, "persistent fast pass C");
-        __shared__ __align__(128) cf lds[B * LdsC::RS];
-        __shared__ cf tw16[kTw16Size];
-        __shared__ unsigned int s_blk[2];
-        const int tid = threadIdx.x;
-        tw16_fill(tw16, tid, T);
-        const uint32_t gx = (uint32_t)(k.N2 / B);
-        const uint32_t per = gx * (uint32_t)k.npairs / 8u;       // blocks per XCD (host: total % 8 == 0)
-        const uint32_t x = blockIdx.x & 7u;                      // this workgroup's XCD (round-robin dispatch)
-        unsigned int *c = ctr + x;
-        if (tid == 0) {
-            s_blk[0] = atomicAdd(c, 1u);
-            s_blk[1] = atomicAdd(c, 1u);
-        }
-        __syncthreads();
-        uint32_t cur = s_blk[0], nxt = s_blk[1];
-        if (cur >= per) return;
-        const int64_t N2 = k.N2;
-        const PssPipeline &p = k.p;
-        const float invN = k.invN, nn = p.noise_norm;
-        const Rng gn(p.seed, p.call_noise, P_NOISE);
-        const uint32_t rbytes = (uint32_t)(k.N * 4);
-        const uint32_t RP = (uint32_t)rpitch(k);
-        const uint32_t pbytes = (uint32_t)(pstride(k) * 8);
-        auto where = [&](uint32_t blk, int &cbx, int &pr) __attribute__((always_inline)) {
-            const uint32_t l = x * per + blk;
-            pr = (int)(l / gx);
-            cbx = (int)(l - (uint32_t)pr * gx);
-        };
-        float4 R[2 * ITEMS];
-        auto load = [&](uint32_t blk, int tl) __attribute__((always_inline)) {
-            int cbx, pr;
-            where(blk, cbx, pr);
-            const Buf Y(k.Yd + (int64_t)pr * pstride(k), pbytes);
-            const uint32_t s0 = (uint32_t)cbx * (uint32_t)B * 8u;
-#pragma unroll
-            for (int t = 0; t < ITEMS; ++t) {
-                const int it = tl + t * T, k1 = it / (B / 4), b4 = (it - k1 * (B / 4)) * 4;
-                const uint32_t off = ((uint32_t)k1 * RP + (uint32_t)b4) * 8u;
-                R[2 * t] = Y.ld4(off, s0);
-                R[2 * t + 1] = Y.ld4(off + 16u, s0);
-            }
-        };
-        load(cur, tid);
-        for (int i = 0;; ++i) {
-            // (opaque per iteration: the loop's address arithmetic is
-            // recomputed instead of hoisted and held live across it -- 128
-            // VGPRs and scratch spills otherwise)
-            const int ti = opaque(tid), li = ti & 63, wi = ti >> 6;
-            int cbx, pr;
-            where(cur, cbx, pr);
-            const int64_t n20 = (int64_t)cbx * B;
-            // the spill block, four-step twiddled (inv_block's values), into LDS
-#pragma unroll
-            for (int t = 0; t < ITEMS; ++t) {
-                const int it = ti + t * T, k1 = it / (B / 4), b4 = (it - k1 * (B / 4)) * 4;
-                const float4 lo = R[2 * t], hi = R[2 * t + 1];
-                const cf a[4] = {make_float2(lo.x, lo.y), make_float2(lo.z, lo.w),
-                                 make_float2(hi.x, hi.y), make_float2(hi.z, hi.w)};
-                const uint32_t m0 = (uint32_t)(n20 + b4) * (uint32_t)k1;
-                float r0 = (float)m0 * invN;
-                if (r0 >= 0.5f) r0 -= 1.0f;
-                float r1 = (float)k1 * invN;
-                if (r1 >= 0.5f) r1 -= 1.0f;
-                const cf w0 = expi_rev(r0), w1 = expi_rev(r1);
-                const cf w2 = cmul(w1, w1);
-                const cf tw[4] = {w0, cmul(w0, w1), cmul(w0, w2), cmul(w0, cmul(w2, w1))};
-#pragma unroll
-                for (int q = 0; q < 4; ++q) lds[LdsC::at(b4 + q, k1)] = cmul(a[q], tw[q]);
-            }
-            __syncthreads();
-#ifndef PSS_PC_PREFETCH_LATE
-            if (nxt < per) load(nxt, opaque(ti));
-#endif
-            if (ti == 0) s_blk[i & 1] = (nxt < per) ? atomicAdd(c, 1u) : per;
-            {
-                cf v[E];
-                cf *wl = lds + wi * LdsC::RS;
-                FW::template load<RI0>(v, wl, li);
-                stage_sync<true>();
-                FW::template run_tw<true, 1, I...>(v, wl, li, tw16);
-                FW::template store<RIL>(v, wl, li);
-            }
-            __syncthreads();
-#ifdef PSS_PC_PREFETCH_LATE
-            if (nxt < per) load(nxt, opaque(ti));
-#endif
-            const int ra = 2 * pr - k.poff, rb = ra + 1;
-            const bool hasa = ra >= 0, hasb = rb < p.nchan;
-            const uint32_t ca = (uint32_t)(p.chan0 + ra), cb = ca + 1u;
-            const Buf oa(p.data + (int64_t)max(ra, 0) * p.ld, rbytes), ob(p.data + (int64_t)min(rb, p.nchan - 1) * p.ld, rbytes);
-#pragma unroll
-            for (int t = 0; t < ITEMS; ++t) {
-                const int it = ti + t * T;
-                const int n1 = it / (B / 4);
-                const int b4 = (it - n1 * (B / 4)) * 4;
-                const uint32_t n = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4;
-                const float4 xa = chi2_1x4(gn.bits(n >> 2, ca, 0u));
-                const float4 xb = chi2_1x4(gn.bits(n >> 2, cb, 0u));
-                const float na[4] = {xa.x, xa.y, xa.z, xa.w}, nb[4] = {xb.x, xb.y, xb.z, xb.w};
-                float A[4], Bv[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const cf z = lds[LdsC::at(b4 + q, n1)];
-                    A[q] = fmaf(nn, na[q], z.x * invN);
-                    Bv[q] = fmaf(nn, nb[q], z.y * invN);
-                }
-                if (hasa) oa.st4(A[0], A[1], A[2], A[3], n * 4u, 0);
-                if (hasb) ob.st4(Bv[0], Bv[1], Bv[2], Bv[3], n * 4u, 0);
-            }
-            __syncthreads();
-            if (nxt >= per) break;
-            cur = nxt;
-            nxt = s_blk[i & 1];
-        }
-    }
-
     __device__ static void passC_fast(const KP &k) {
         static_assert(kItemsExact, "fast pass C: whole items per thread");
         __shared__ __align__(128) cf lds[B * LdsC::RS];
@@ -2320,8 +2193,6 @@ template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairC(KP k) { C::passC(k); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairC_fast(KP k) { C::passC_fast(k); }
-template <typename C, int T>
-__global__ __launch_bounds__(T) void k_pairC_fast_persist(KP k, unsigned int *ctr) { C::passC_fast_persist(k, ctr); }
 template <typename C, int T>
 __global__ __launch_bounds__(T, T == 512 ? 2 : 4) void k_pairC_fast32(KP k) { C::passC_fast32(k); }
 template <typename C, int T>
@@ -2487,7 +2358,6 @@ static inline BsGeom bs_geom(int32_t nchan, int64_t N) {
 
 struct WsLayout {
     int64_t yd, mspec, ynode, nodes, bits, base, coef, misc, mbits, rtab, wlist, row, total;
-    int64_t pcnt;                      // persistent pass C: per-XCD block counters (8 x u32)
     int64_t bs_chirp, bs_bhat, bs_z;   // Bluestein: w [N] | Bhat [M] | Z [nb][M] (cf)
     int64_t odd_tw;                    // odd N: exp(+2 pi i j / (N - 1)), j < N - 1 (cf)
     int64_t rf_tw, rf_B, rf_mx;        // float64 null decisions: e^{2 pi i n/N} [N], B [N/2+1] (double2), row max [nchan]
@@ -2513,7 +2383,6 @@ static inline WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
         w.mbits = o; o += al256((int64_t)nchan * (N / 8));   // per-channel null bits
         w.rtab = o;  o += al256(npairs * 2 * 64 * 8);          // row-pass pair ramp factors (RFL <= 64)
         w.wlist = o; o += al256((N / 32) * 4);                 // null fix-up: table words with nulls
-        w.pcnt = o;  o += 256;                                  // persistent pass C counters
     } else if (!filt && is_pow2(N) && N >= 64 && N <= 8192) {
         // single-workgroup lengths: W1 [nchan][N] cf and the float64 null
         // refine's buffers (a delayed null: run_single)
@@ -2762,26 +2631,6 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
     return launch_pair_passes<N1, B, T, CF, CI, N2, TR, RF, RI, TRF, BC, TC>(k, st);
 }
 
-// CUs of the current device (the persistent pass C's grid)
-static inline int device_cus() {
-    static int cus[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus[dev] = 256;
-    return cus[dev] > 0 ? cus[dev] : 256;
-}
-// the persistent fast pass C (PairCols::passC_fast_persist): C3's 16-column
-// blocks of 1024-point columns, a block count the 8 XCD ranges split evenly,
-// and more blocks than workgroups
-static inline bool pc_persist(const KP &k, int64_t gx) {
-#ifdef PSS_NO_PC_PERSIST
-    return false;
-#endif
-    const int64_t total = gx * (int64_t)k.npairs;
-    return (total % 8) == 0 && total >= 8 * (int64_t)device_cus();
-}
-
 // The passes of one pair range (after the mask table and the ramp table).
 template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typename RF, typename RI,
           int TRF, int BC, int TC>
@@ -2857,22 +2706,8 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
                     <<<dim3((unsigned)(N2 / 16), (unsigned)k.npairs), dim3(512), 0, st>>>(k);
                 plan_note(" C:fast32");
             } else {
-                bool done = false;
-                if constexpr (N1 == 1024 && BC == 16 && TC == 1024) {
-                    if (pc_persist(k, N2 / BC)) {
-                        // one workgroup per CU walking its XCD's column blocks
-                        unsigned int *ctr = reinterpret_cast<unsigned int *>(reinterpret_cast<char *>(k.p.work) +
-                                                                             ws_layout(k.p.nchan, k.N).pcnt);
-                        HIPCHK(hipMemsetAsync(ctr, 0, 8 * sizeof(unsigned int), st));
-                        k_pairC_fast_persist<PCC, TC><<<dim3((unsigned)device_cus()), dim3(TC), 0, st>>>(k, ctr);
-                        plan_note(" C:fast_persist");
-                        done = true;
-                    }
-                }
-                if (!done) {
-                    k_pairC_fast<PCC, TC><<<dim3((unsigned)(N2 / BC), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
-                    plan_note(" C:fast");
-                }
+                k_pairC_fast<PCC, TC><<<dim3((unsigned)(N2 / BC), (unsigned)k.npairs), dim3(TC), 0, st>>>(k);
+                plan_note(" C:fast");
             }
         }
     } else if (PC::kRegCols && fold_epilogue(k)) {

@@ -51,8 +51,7 @@ def test_workspace_sizes():
     # complex per pair) + the null fix-up's word list (N/32 u32) + mask row -- no
     # per-channel mask spill
     table = n * 8 + 6 * n * 8 + 12 * n * 4 + (n // 32) * 8 + (n // 32) * 4 + n * 16 * 4 + 256
-    # (+ round 6: the persistent pass C's 8 per-XCD block counters, 256 B)
-    wl = (n // 32) * 4 + 256
+    wl = (n // 32) * 4
     assert L.pss_workspace_bytes(4, n) == 3 * n * 8 + table + 4 * n // 8 + 3 * 1024 + wl + n * 4
     assert L.pss_workspace_bytes(3, n) == 2 * n * 8 + table + 3 * n // 8 + 2 * 1024 + wl + n * 4
     a = lambda b: ((b + 255) // 256) * 256

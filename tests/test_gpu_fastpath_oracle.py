@@ -77,8 +77,7 @@ GEOMS = {"c3": (22, 2048, True, 100, True), "c5": (24, 8192, False, 500, False),
          "c5_null": (24, 8192, False, 500, True)}
 # the kernels each geometry must run (pss_plan_collect tokens)
 PLANS = {"c3": ("fourstep", "1024x4096", "A:fast", "R:pair_row", "C:fast", "N:table", "N:fix_list"),
-         # (4 channels of 2^24: 2048 column blocks, the persistent pass C)
-         "c5": ("fourstep", "1024x16384", "A:fast_shared", "R:pair_row_seq", "C:fast_persist"),
+         "c5": ("fourstep", "1024x16384", "A:fast_shared", "R:pair_row_seq", "C:fast"),
          "c5_null": ("fourstep", "2048x8192", "A:fast_shared", "R:pair_row_seq", "C:fast32", "N:table",
                      "N:fix_list")}
 

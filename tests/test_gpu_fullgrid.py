@@ -69,15 +69,13 @@ def _check_grid(nchan, log2n, c3, blocks, plan):
 
 def test_c3_full_grid_rows_match_shards(hip_lib):
     """C3: 2048 x 2^22, scatter + DM 100 + null(0.1) + noise (1024 x 4096:
-    k_pairA_fast, k_pair_row, the persistent k_pairC_fast_persist, the mask
-    table and k_null_fix_list; the 4-channel shard runs take k_pairC_fast,
-    so their bitwise equality is also persistent == one-block-per-workgroup)."""
+    k_pairA_fast, k_pair_row, k_pairC_fast, the mask table and k_null_fix_list)."""
     _check_grid(2048, 22, True, [(0, 4), (1022, 1026), (2044, 2048)],
-                ("fourstep", "1024x4096", "A:fast", "R:pair_row", "C:fast_persist", "N:table", "N:fix_list"))
+                ("fourstep", "1024x4096", "A:fast", "R:pair_row", "C:fast", "N:table", "N:fix_list"))
 
 
 def test_c5_full_grid_rows_match_shards(hip_lib):
     """C5 per GPU: 1024 x 2^24, DM 500 + noise (no null: the 1024 x 16384
     split -- C3's column kernels and the 16384-point k_pair_row_seq)."""
     _check_grid(1024, 24, False, [(0, 2), (510, 514), (1020, 1024)],
-                ("fourstep", "1024x16384", "A:fast_shared", "R:pair_row_seq", "C:fast_persist"))
+                ("fourstep", "1024x16384", "A:fast_shared", "R:pair_row_seq", "C:fast"))
