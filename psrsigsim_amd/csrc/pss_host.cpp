@@ -18,7 +18,12 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -38,23 +43,87 @@ inline double edge_slope(double h0, double h1, double m0, double m1) {
     return (!flip && big) ? 3.0 * m0 : d;
 }
 
+// A persistent pool of host threads for the row passes: starting and joining
+// std::threads costs ~20-100 us each per call, more than a share of these
+// passes on a 2048-row table (two or three calls per signal).  Workers are
+// started once (lazily, and again in a forked child: the pool records its
+// pid), then wait for row blocks.
+class Pool {
+  public:
+    void run(int64_t rows, int nt, const std::function<void(int64_t, int64_t)> &fn) {
+        std::lock_guard<std::mutex> one(run_mu_);   // one pass at a time (callers on several threads)
+        std::unique_lock<std::mutex> lk(mu_);
+        ensure(nt - 1);
+        fn_ = &fn;
+        rows_ = rows;
+        nt_ = nt;
+        next_ = 1;                     // block 0 runs on the calling thread
+        done_ = 0;
+        ++gen_;
+        cv_.notify_all();
+        lk.unlock();
+        fn(0, rows / nt);
+        lk.lock();
+        done_cv_.wait(lk, [&] { return done_ == nt_ - 1; });
+        fn_ = nullptr;
+    }
+
+  private:
+    void ensure(int workers) {
+        if (pid_ != getpid()) {        // a forked child: the parent's workers do not exist here
+            for (auto &t : th_) t.detach();
+            th_.clear();
+            pid_ = getpid();
+        }
+        while ((int)th_.size() < workers) th_.emplace_back([this] { loop(); });
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        const pid_t me = pid_;
+        for (;;) {
+            cv_.wait(lk, [&] { return gen_ != seen && fn_ && next_ < nt_; });
+            if (pid_ != me) return;
+            const int b = next_++;
+            if (next_ >= nt_) seen = gen_;
+            const int64_t a = rows_ * b / nt_, e = rows_ * (b + 1) / nt_;
+            const std::function<void(int64_t, int64_t)> *fn = fn_;
+            lk.unlock();
+            (*fn)(a, e);
+            lk.lock();
+            if (++done_ == nt_ - 1) done_cv_.notify_one();
+        }
+    }
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_cv_;
+    std::vector<std::thread> th_;
+    const std::function<void(int64_t, int64_t)> *fn_ = nullptr;
+    int64_t rows_ = 0;
+    int nt_ = 0, next_ = 0, done_ = 0;
+    uint64_t gen_ = 0;
+    pid_t pid_ = 0;
+};
+
+Pool &pool() {
+    static Pool *p = new Pool();       // (never destroyed: workers may outlive static teardown)
+    return *p;
+}
+
 template <typename F>
 void parallel_rows(int64_t rows, int nthreads, F fn) {
     if (nthreads <= 1 || rows < 512) {
         fn(0, rows);
         return;
     }
-    // >= 256 rows per thread: a thread costs ~50-100 us to start and join,
-    // more than a 256-row share of these passes (make_pulses at 256 channels
-    // x 244 phases: 3.3 ms on one thread, 5.7 on eight, this container)
+    // >= 256 rows per block (make_pulses at 256 channels x 244 phases: one
+    // block on one thread beats splitting it)
     const int nt = (int)std::min<int64_t>(nthreads, rows / 256);
-    std::vector<std::thread> th;
-    th.reserve(nt);
-    for (int t = 0; t < nt; ++t) {
-        const int64_t a = rows * t / nt, b = rows * (t + 1) / nt;
-        th.emplace_back([=] { fn(a, b); });
+    if (nt <= 1) {
+        fn(0, rows);
+        return;
     }
-    for (auto &x : th) x.join();
+    const std::function<void(int64_t, int64_t)> f = fn;
+    pool().run(rows, nt, f);
 }
 
 }  // namespace

@@ -232,8 +232,11 @@ class Pulsar(object):
             rand_pulses = _engine.host_rng(call).choice(signal.nsub, null_pulses, replace=False)
         rand_pulses = np.asarray(rand_pulses, dtype=np.int64)
         rank = np.full(max(int(signal.nsub), 1), -1, dtype=np.int32)
-        for r, p in enumerate(rand_pulses):
-            rank[p] = r
+        if np.unique(rand_pulses).size == rand_pulses.size:
+            rank[rand_pulses] = np.arange(rand_pulses.size, dtype=np.int32)
+        else:
+            for r, p in enumerate(rand_pulses):      # repeats: the later entry wins, as there
+                rank[p] = r
         opm = float(np.mean(self.Profiles._max_profile[opw.astype(int)]))
         dn = float(signal._draw_norm)
         st = {"rank": rank, "shift_dev": shift_dev, "nph": Nph, "call_id": call,
