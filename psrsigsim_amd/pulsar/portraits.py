@@ -392,7 +392,8 @@ class DataPortrait(PulsePortrait):
         x = self._knots
         nint = x.size - 1
         M = int(round(1.0 / (x[1] - x[0]))) if nint >= 1 else 0
-        if M < 1 or not np.allclose(x, np.arange(x.size) / M, rtol=0, atol=1e-15):
+        # (allclose(x, arange / M, rtol=0, atol=1e-15), without its temporaries)
+        if M < 1 or not np.max(np.abs(x - np.arange(x.size) / M)) <= 1e-15:
             return None
         return M, nint
 

@@ -283,7 +283,15 @@ def _device_table(portrait):
         from .portraits import rows_of
         h = 1.0 / M
         amax = portrait.Amax if hasattr(portrait, '_Amax') else 1.0
-        c = np.asarray(rows_of(portrait._coef), dtype=np.float64)[:, nint - 1, :]
+        x = portrait._knots
+        if getattr(portrait, "_coef_cache", None) is None and x.size >= 4:
+            # the last piece only: its slopes come from the last four knots
+            # (an interior slope and the end slope), so the PCHIP through
+            # those gives that piece bit for bit without fitting every interval
+            from .portraits import pchip_coefficients
+            c = np.asarray(pchip_coefficients(x[-4:], rows_of(portrait._kvals)[:, -4:]), dtype=np.float64)[:, -1, :]
+        else:
+            c = np.asarray(rows_of(portrait._coef), dtype=np.float64)[:, nint - 1, :]
         d3, d2, d1, d0 = (c[:, 0] * h ** 3 / amax, c[:, 1] * h ** 2 / amax, c[:, 2] * h / amax, c[:, 3] / amax)
         ext = []
         for m in range(1, M - nint + 1):
