@@ -134,31 +134,81 @@ extern "C" {
 
 namespace {
 
-// One row's PCHIP coefficients (the NumPy statement's operations, in order):
-// m, d (slopes) are scratch of K - 1 and K; cr receives (K - 1) x 4.
-inline void pchip_row(const double *h, int64_t K, const double *yr, double *m, double *d, double *cr) {
-    for (int64_t i = 0; i + 1 < K; ++i) m[i] = (yr[i + 1] - yr[i]) / h[i];
+// The PCHIP coefficients of the intervals [a, b) of one row (0 <= a < b <=
+// K - 1): the NumPy statement's operations restricted to that range (secants
+// m over [a - 1, b], slopes d over [a, b]), so a row cut into spans gives the
+// bits of the whole-row pass.  mm / dd: scratch of >= b - a + 2 and b - a + 1;
+// cr receives (b - a) x 4.  The interior slope is computed on flat knots too
+// and then discarded (a select instead of a branch, so the loop vectorises;
+// the kept values are the same operations).
+inline void pchip_span(const double *h, int64_t K, const double *yr, int64_t a, int64_t b, double *mm,
+                       double *dd, double *cr) {
+    const int64_t ma = a > 0 ? a - 1 : 0, mb = std::min<int64_t>(b + 1, K - 1);
+    for (int64_t i = ma; i < mb; ++i) mm[i - ma] = (yr[i + 1] - yr[i]) / h[i];
     if (K == 2) {
-        d[0] = d[1] = m[0];
+        dd[0] = dd[1] = mm[0];
     } else {
-        for (int64_t i = 1; i + 1 < K; ++i) {
-            const double m0 = m[i - 1], m1 = m[i];
+        const int64_t ia = std::max<int64_t>(a, 1), ib = std::min<int64_t>(b, K - 2);
+        for (int64_t i = ia; i <= ib; ++i) {
+            const double m0 = mm[i - 1 - ma], m1 = mm[i - ma];
             const double w1 = 2.0 * h[i] + h[i - 1];
             const double w2 = h[i] + 2.0 * h[i - 1];
             const bool flat = (std::signbit(m0) != std::signbit(m1)) || (m1 == 0.0) || (m0 == 0.0);
-            d[i] = flat ? 0.0 : 1.0 / ((w1 / m0 + w2 / m1) / (w1 + w2));
+            const double v = 1.0 / ((w1 / m0 + w2 / m1) / (w1 + w2));
+            dd[i - a] = flat ? 0.0 : v;
         }
-        d[0] = edge_slope(h[0], h[1], m[0], m[1]);
-        d[K - 1] = edge_slope(h[K - 2], h[K - 3], m[K - 2], m[K - 3]);
+        if (a == 0) dd[0] = edge_slope(h[0], h[1], mm[0 - ma], mm[1 - ma]);
+        if (b == K - 1) dd[b - a] = edge_slope(h[K - 2], h[K - 3], mm[K - 2 - ma], mm[K - 3 - ma]);
     }
-    for (int64_t i = 0; i + 1 < K; ++i) {
-        const double d0 = d[i], d1 = d[i + 1], hi = h[i], mi = m[i];
+    for (int64_t i = a; i < b; ++i) {
+        const double d0 = dd[i - a], d1 = dd[i + 1 - a], hi = h[i], mi = mm[i - ma];
         const double t = (d0 + d1 - 2.0 * mi) / hi;
-        cr[4 * i + 0] = t / hi;
-        cr[4 * i + 1] = (mi - d0) / hi - t;
-        cr[4 * i + 2] = d0;
-        cr[4 * i + 3] = yr[i];
+        double *c = cr + 4 * (i - a);
+        c[0] = t / hi;
+        c[1] = (mi - d0) / hi - t;
+        c[2] = d0;
+        c[3] = yr[i];
     }
+}
+
+// One row's PCHIP coefficients: m, d scratch of K - 1 and K; cr (K - 1) x 4.
+inline void pchip_row(const double *h, int64_t K, const double *yr, double *m, double *d, double *cr) {
+    pchip_span(h, K, yr, 0, K - 1, m, d, cr);
+}
+
+// Per-thread scratch rows (reused across calls: no allocation per row).
+inline double *scratch(int which, int64_t n) {
+    static thread_local std::vector<double> buf[3];
+    if ((int64_t)buf[which].size() < n) buf[which].resize(n);
+    return buf[which].data();
+}
+
+// fn(r, a, b) over spans [a, b) of the K - 1 intervals of each of `rows`
+// rows, on the host threads when there is enough work (as parallel_rows:
+// >= 256 rows per block for a many-row table; a few long rows -- a 48 828-
+// phase tutorial profile -- are cut into spans of >= 4096 intervals).
+template <typename F>
+void parallel_spans(int64_t rows, int64_t K, int nthreads, F fn) {
+    const int64_t nint = K - 1;
+    int64_t S = 1;
+    int nt = 1;
+    if (nthreads > 1 && rows >= nthreads) {
+        nt = rows >= 512 ? (int)std::min<int64_t>(nthreads, rows / 256)
+                         : (rows * nint >= 131072 ? nthreads : 1);   // (256 x 244: one thread is faster)
+    } else if (nthreads > 1 && rows >= 1) {
+        S = std::max<int64_t>(1, std::min<int64_t>((nthreads + rows - 1) / rows, nint / 4096));
+        nt = (int)std::min<int64_t>(nthreads, rows * S);
+        if (S == 1) nt = 1;
+    }
+    const int64_t tasks = rows * S;
+    const std::function<void(int64_t, int64_t)> f = [&](int64_t t0, int64_t t1) {
+        for (int64_t t = t0; t < t1; ++t) {
+            const int64_t r = t / S, q = t % S;
+            fn(r, nint * q / S, nint * (q + 1) / S);
+        }
+    };
+    if (nt <= 1) f(0, tasks);
+    else pool().run(tasks, nt, f);
 }
 
 // interval = last breakpoint <= phase (searchsorted 'right' - 1), clipped to
@@ -193,9 +243,9 @@ int pss_host_pchip_coef(const double *x, int64_t K, const double *y, int64_t row
     if (K < 2 || rows < 0 || !x || !y || !c) return PSS_EINVAL;
     std::vector<double> h(K - 1);
     for (int64_t i = 0; i + 1 < K; ++i) h[i] = x[i + 1] - x[i];
-    parallel_rows(rows, nthreads, [&](int64_t r0, int64_t r1) {
-        std::vector<double> m(K - 1), d(K);
-        for (int64_t r = r0; r < r1; ++r) pchip_row(h.data(), K, y + r * K, m.data(), d.data(), c + r * (K - 1) * 4);
+    parallel_spans(rows, K, nthreads, [&](int64_t r, int64_t a, int64_t b) {
+        double *m = scratch(0, b - a + 2), *d = scratch(1, b - a + 1);
+        pchip_span(h.data(), K, y + r * K, a, b, m, d, c + (r * (K - 1) + a) * 4);
     });
     return PSS_OK;
 }
@@ -236,16 +286,14 @@ int pss_host_pchip_table(const double *x, int64_t K, const double *y, int64_t ro
     for (int64_t i = 0; i + 1 < K; ++i) h[i] = x[i + 1] - x[i];
     const double w[4] = {pow(hcell, 3.0), pow(hcell, 2.0), hcell, 1.0};
     const bool dv = amax != 1.0;
-    parallel_rows(rows, nthreads, [&](int64_t r0, int64_t r1) {
-        std::vector<double> m(K - 1), d(K), cr((K - 1) * 4);
-        for (int64_t r = r0; r < r1; ++r) {
-            pchip_row(h.data(), K, y + r * K, m.data(), d.data(), cr.data());
-            float *o = out + r * (K - 1) * 4;
-            for (int64_t e = 0; e < (K - 1) * 4; ++e) {
-                double v = cr[e] * w[e & 3];
-                if (dv) v = v / amax;
-                o[e] = (float)v;
-            }
+    parallel_spans(rows, K, nthreads, [&](int64_t r, int64_t a, int64_t b) {
+        double *m = scratch(0, b - a + 2), *d = scratch(1, b - a + 1), *cr = scratch(2, (b - a) * 4);
+        pchip_span(h.data(), K, y + r * K, a, b, m, d, cr);
+        float *o = out + (r * (K - 1) + a) * 4;
+        for (int64_t e = 0; e < (b - a) * 4; ++e) {
+            double v = cr[e] * w[e & 3];
+            if (dv) v = v / amax;
+            o[e] = (float)v;
         }
     });
     return PSS_OK;

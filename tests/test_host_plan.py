@@ -272,18 +272,51 @@ def test_native_device_table_bitwise():
 
 
 def test_native_threads_invariant():
-    import os
+    """The row passes' results do not depend on the thread count (the count
+    goes to the native call directly: _lib.host_threads() is read once)."""
     from psrsigsim_amd import _lib
+    L = _lib.load()
     x, y = _pchip_cases()[0]
-    old = os.environ.get("PSS_HOST_THREADS")
-    try:
-        os.environ["PSS_HOST_THREADS"] = "1"
-        a = _lib.host_pchip_coef(x, y)
-        os.environ["PSS_HOST_THREADS"] = "7"
-        b = _lib.host_pchip_coef(x, y)
-    finally:
-        if old is None:
-            os.environ.pop("PSS_HOST_THREADS", None)
-        else:
-            os.environ["PSS_HOST_THREADS"] = old
-    np.testing.assert_array_equal(a, b)
+    y = np.repeat(y, 4, axis=0)            # 1200 rows: the row-block path
+    outs = []
+    for nt in (1, 7):
+        c = np.empty((y.shape[0], x.size - 1, 4))
+        _lib.check(L.pss_host_pchip_coef(_lib._dptr(x), x.size, _lib._dptr(y), y.shape[0], _lib._dptr(c), nt),
+                   "coef")
+        outs.append(c)
+    np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def _long_rows():
+    rng = np.random.default_rng(11)
+    K = 48829                              # the tutorial-1 profile's phase count + 1
+    x = np.arange(K) / (K - 1.0)
+    y = rng.random((3, K))
+    y[0, 1000:9000] = 0.5                  # a flat run across span boundaries
+    y[1] = np.sin(np.linspace(0, 40, K))   # sign changes
+    y[2, 6000:6300] = 0.0
+    return x, y
+
+
+@pytest.mark.parametrize("rows", [1, 3])
+def test_native_pchip_long_rows_spans_bitwise(rows):
+    """A few long rows are cut into spans over the host threads
+    (pss_host.cpp parallel_spans): coefficients and the fused device table
+    equal the NumPy statement bit for bit at any thread count."""
+    from psrsigsim_amd import _lib
+    from psrsigsim_amd.pulsar.portraits import pchip_coefficients_np
+    L = _lib.load()
+    x, y = _long_rows()
+    y = np.ascontiguousarray(y[:rows])
+    K = x.size
+    c_np = pchip_coefficients_np(x, y)
+    h = 1.0 / (K - 1)
+    for nt in (1, 3, 8):
+        c = np.empty_like(c_np)
+        _lib.check(L.pss_host_pchip_coef(_lib._dptr(x), K, _lib._dptr(y), rows, _lib._dptr(c), nt), "coef")
+        np.testing.assert_array_equal(c, c_np)
+        for amax in (1.0, 0.7316):
+            t = np.empty((rows, K - 1, 4), np.float32)
+            _lib.check(L.pss_host_pchip_table(_lib._dptr(x), K, _lib._dptr(y), rows, h, amax, _lib._dptr(t), nt),
+                       "table")
+            np.testing.assert_array_equal(t, _lib.host_device_table(c_np, h, amax))
