@@ -256,15 +256,22 @@ def host_pchip_eval(x, y, ph, div=1.0):
     return out
 
 
-def host_pchip_table(x, y, h, amax):
-    """pchip_coefficients then host_device_table, fused per row."""
+def host_pchip_table(x, y, h, amax, width=None):
+    """pchip_coefficients then host_device_table, fused per row.  ``width``
+    (> K - 1, one row): the table is allocated with that many intervals and
+    the first K - 1 filled (the caller completes the rest in place)."""
     import numpy as np
     x = np.ascontiguousarray(x, dtype=np.float64)
     y = np.ascontiguousarray(y, dtype=np.float64)
-    out = np.empty((y.shape[0], x.size - 1, 4), dtype=np.float32)
+    n = x.size - 1
+    if width is not None and width > n and y.shape[0] == 1:
+        buf = np.empty((1, width, 4), dtype=np.float32)
+        out = buf[:, :n]                   # (one row: contiguous)
+    else:
+        buf = out = np.empty((y.shape[0], n, 4), dtype=np.float32)
     check(load().pss_host_pchip_table(_dptr(x), x.size, _dptr(y), y.shape[0], float(h), float(amax),
                                       _dptr(out), host_threads()), "pss_host_pchip_table")
-    return out
+    return buf
 
 
 def host_device_table(c, h, amax):

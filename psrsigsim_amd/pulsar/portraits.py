@@ -235,9 +235,19 @@ class PulsePortrait(object):
 
 
 def _gauss_single(ph, peak, width, amp):
-    if np.any(ph > 1) or np.any(ph < 0):
+    ph = np.asarray(ph)
+    if ph.size and (ph.max() > 1 or ph.min() < 0):      # (np.any(ph > 1) or np.any(ph < 0): NaN passes both)
         raise ValueError('Phase values must all lie within [0,1].')
-    return amp * np.exp(-0.5 * ((ph - peak) / width) ** 2)
+    t = (ph - peak) / width
+    if t.dtype != np.float64 or np.ndim(amp) or np.ndim(t) == 0:
+        return amp * np.exp(-0.5 * t ** 2)
+    # amp * exp(-0.5 * t ** 2) in place (t ** 2 is np.square; the same
+    # operations and bits, two temporaries fewer on a 48 828-phase profile)
+    np.square(t, out=t)
+    t *= -0.5
+    np.exp(t, out=t)
+    t *= amp
+    return t
 
 
 def _gauss_sum(ph, peaks, widths, amps):
@@ -320,6 +330,7 @@ class DataPortrait(PulsePortrait):
         def band_any(flags):
             f = bool(np.any(flags))
             return f if rowset is None else rowset.any(f)
+        self._geo = None
         if phases is None:
             N = work.shape[1]
             if band_any(work[:, 0] != work[:, -1]):
@@ -327,6 +338,8 @@ class DataPortrait(PulsePortrait):
                 phases = np.arange(N + 1) / N
             else:
                 phases = np.arange(N) / N
+            if phases.size >= 2:
+                self._geo = (N, phases.size - 1)   # knots k / N: uniform_knots' answer
         else:
             phases = np.asarray(phases, dtype=float)
             if phases[-1] != 1:
@@ -389,6 +402,8 @@ class DataPortrait(PulsePortrait):
     # -- device export --------------------------------------------------
     def uniform_knots(self):
         """(M, nint) when the knots are k/M (k = 0..nint), else None."""
+        if getattr(self, "_geo", None) is not None:
+            return self._geo
         x = self._knots
         nint = x.size - 1
         M = int(round(1.0 / (x[1] - x[0]))) if nint >= 1 else 0
@@ -397,12 +412,15 @@ class DataPortrait(PulsePortrait):
             return None
         return M, nint
 
-    def device_table(self):
+    def device_table(self, room=False):
         """float32 [rows, nint, 4] coefficients in the local coordinate
         u = (phase - k/M) * M, ordered (u^3, u^2, u^1, u^0), divided by Amax
         so the device evaluates calc_profiles directly; plus (M, nint).  On
         non-uniform knots see :meth:`split_table` (the third element is then
-        the [M] split points instead of nint, and the table is [rows, M, 8])."""
+        the [M] split points instead of nint, and the table is [rows, M, 8]).
+        ``room``: a one-row table whose knots stop short of the period may come
+        back M intervals wide, the last M - nint left for the caller
+        (pulsar._device_table's extrapolated pieces)."""
         geo = self.uniform_knots()
         if geo is None:
             return self.split_table()
@@ -413,7 +431,8 @@ class DataPortrait(PulsePortrait):
         # (one row for a uniform table: the device then shares it); straight
         # from the knot values when no coefficient table exists yet
         if self._coef_cache is None:
-            return _lib.host_pchip_table(self._knots, rows_of(self._kvals), h, amax), M, nint
+            return _lib.host_pchip_table(self._knots, rows_of(self._kvals), h, amax,
+                                         width=M if room else None), M, nint
         return _lib.host_device_table(np.ascontiguousarray(rows_of(self._coef)), h, amax), M, nint
 
 

@@ -275,7 +275,7 @@ def _device_table(portrait):
     intervals k = nint .. M-1 get that cubic re-expanded in their own local
     coordinate, c(u + m) with m = k - nint + 1, in float64.  The kernels then
     need no extrapolation branch per sample."""
-    tab, M, third = portrait.device_table()
+    tab, M, third = portrait.device_table(room=True)
     if np.ndim(third) == 1:
         return tab, M, M, np.asarray(third, dtype=np.float32)
     nint = int(third)
@@ -297,8 +297,11 @@ def _device_table(portrait):
         for m in range(1, M - nint + 1):
             ext.append(np.stack([d3, 3 * d3 * m + d2, (3 * d3 * m + 2 * d2) * m + d1,
                                  ((d3 * m + d2) * m + d1) * m + d0], axis=-1))
-        tab = np.concatenate([np.asarray(tab, dtype=np.float32),
-                              np.stack(ext, axis=1).astype(np.float32)], axis=1)
+        ext = np.stack(ext, axis=1).astype(np.float32)
+        if np.shape(tab)[1] == M:
+            tab[:, nint:, :] = ext         # (the table came with room for them)
+        else:
+            tab = np.concatenate([np.asarray(tab, dtype=np.float32), ext], axis=1)
     return tab, M, M, None
 
 

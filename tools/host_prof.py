@@ -1,5 +1,5 @@
 """Host-side profile (cProfile) of a bench workload step on the GPU box:
-where the non-kernel time of a step goes.  usage: tools/host_prof.py c4|c3|t1|t2"""
+where the non-kernel time of a step goes.  usage: tools/host_prof.py c4|c3|t1|t2 [steps]"""
 import cProfile
 import pstats
 import sys
@@ -21,10 +21,13 @@ torch.cuda.synchronize()
 pr = cProfile.Profile()
 t = time.perf_counter()
 pr.enable()
-for _ in range(5):
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+for _ in range(N):
     s = step()
-    s.data
+    if wl != "c3":
+        s.data
 torch.cuda.synchronize()
 pr.disable()
-print("ms/step %.2f" % ((time.perf_counter() - t) / 5 * 1e3))
-pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+print("ms/step %.2f (under cProfile)" % ((time.perf_counter() - t) / N * 1e3))
+pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+pstats.Stats(pr).sort_stats("cumtime").print_stats(30)
