@@ -20,3 +20,7 @@ for nc in 256 512; do
     || { echo "nchan $nc failed"; tail -3 $OUT/bench_n$nc.err; exit 1; }
   python -c "import json; d=json.loads(open('$OUT/bench_n$nc.json').read().strip().splitlines()[-1]); print('n$nc', d['ms_per_step'], 'first', d['step_ms_first'], 'steady', d['step_ms_steady'])"
 done
+# the first timed step on an idle GPU, decomposed (host planning, the step's
+# own kernels against the steady state's, tools/first_step.py)
+timeout -k 10 200 python tools/first_step.py 2048 2 > $OUT/first_step.txt 2>&1 || { echo "first_step failed"; exit 1; }
+grep "step [01] " $OUT/first_step.txt
