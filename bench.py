@@ -324,12 +324,33 @@ def dry_step(pss, nchan_total, shard, nsamp_log2, plan_group=None):
 
 
 def usable_cores():
-    """CPUs this process may run on (its affinity set: the box's share of a
-    many-core host), next to os.cpu_count() (the whole machine)."""
+    """CPUs this process may use: its affinity set, capped by the cgroup's
+    CPU quota (cgroup v2 cpu.max "quota period", or v1 cfs_quota/period) --
+    the box's share of a many-core host is a quota, not an affinity mask --
+    next to os.cpu_count() (the whole machine)."""
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        return os.cpu_count()
+        n = os.cpu_count() or 1
+    q = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            a, b = f.read().split()[:2]
+            if a != "max":
+                q = float(a) / float(b)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                a = float(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                b = float(f.read())
+            if a > 0:
+                q = a / b
+        except (OSError, ValueError):
+            pass
+    if q is not None:
+        n = min(n, max(1, int(round(q))))
+    return n
 
 
 def cpu_baseline(nch, nsamp_log2):
@@ -783,12 +804,12 @@ def main():
         if args.cpu_workers > 0:
             va, dta = cpu_baseline_allcore(args.cpu_workers, 2, args.log2n)
             cpu_all = {"value": round(va, 1), "unit": "channel-samples/s", "cores": args.cpu_workers,
-                       "cpu_count": os.cpu_count(), "usable_cores": usable_cores(), "kind": "port",
+                       "cpu_count": os.cpu_count(), "usable_cores": usable_cores(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "kind": "port",
                        "sample": "%d concurrent single-threaded processes x 2 ch x 2^%d samp of the same C3 "
                                  "pipeline (oracle/pss_cpu.py), slowest worker %.1f s" % (args.cpu_workers,
                                                                                          args.log2n, dta)}
         cpu = {"value": round(v, 1), "unit": "channel-samples/s", "cores": 1, "cpu_count": os.cpu_count(),
-               "usable_cores": usable_cores(), "kind": "port",
+               "usable_cores": usable_cores(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "kind": "port",
                "sample": "%d ch x 2^%d samp of the same C3 pipeline, oracle/pss_cpu.py (float64 NumPy, "
                          "reference call structure; like the reference it also builds observe's pre-noise "
                          "out copy, ~2%% of its time, which the GPU run elides when ret_resampsig=False), "
@@ -807,7 +828,7 @@ def main():
             c = cpu_tutorial(args.workload, total)
             tut["cpu_oracle"] = {"disperse_only": round(c["disperse"], 1), "disperse_s": round(c["disperse_s"], 3),
                                  "pipeline": round(c["pipeline"], 1), "pipeline_s": round(c["pipeline_s"], 3),
-                                 "cores": 1, "cpu_count": os.cpu_count(), "usable_cores": usable_cores(),
+                                 "cores": 1, "cpu_count": os.cpu_count(), "usable_cores": usable_cores(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
                                  "kind": "port", "host": cpu_model()}
             tut["gpu_disperse_only"]["vs_cpu_oracle"] = round(gv / c["disperse"], 1)
     if rank == 0:
