@@ -96,6 +96,9 @@ struct KP {
     // inverse transform's (data, mask) pairs go to this [nchan][N] buffer
     // (the packed paths' W1) instead of through the epilogue
     cf *w1_out;
+    // shared-profile fast pass A: the pulse profile at every sample, in the
+    // pass's item order (k_prof_cols, PairCols::prof_cols)
+    const float4 *pcol;
 };
 // pair spill row pitch and per-pair stride (complex)
 __host__ __device__ __forceinline__ int64_t rpitch(const KP &k) { return k.N2; }
@@ -129,6 +132,11 @@ static constexpr int KREC = 16;
 // PCHIP intervals the fast pass A keeps in LDS (two rows; 69.7 KB FFT buffer +
 // 12 KB still allows two 512-thread workgroups per CU).
 static constexpr int kFastNint = 376;
+// shared-profile fast pass A reads the per-run sample table (PairCols::prof_cols)
+#ifndef PSS_PCOL
+#define PSS_PCOL 1
+#endif
+static constexpr bool kPcol = PSS_PCOL != 0;
 
 // t = 2 f - 1 and i from the mask ramp word w = frac(s / N) 2^64 (N = 2^L)
 __device__ __forceinline__ void mask_split(uint64_t w, int L, uint32_t &ishift, float &t) {
@@ -1561,6 +1569,55 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
                                      : ((160 * 1024 / (N1 * 8 * B)) * B / 256 > 4 ? 4 : (160 * 1024 / (N1 * 8 * B)) * B / 256);
     static_assert(B % 4 == 0, "4-sample items");
 
+    // Pass A's 4-sample item it of a column block: row n1, first column b4.
+    // Lanes = consecutive rows n1 (of one 4-column group where N1 % 64 == 0):
+    // the transposed LDS writes are conflict-free.
+    __device__ static __forceinline__ void item_of(int it, int &n1, int &b4) {
+        if constexpr (N1 % 64 == 0) {
+            n1 = it % N1;
+            b4 = (it / N1) * 4;
+        } else {
+            n1 = it / (B / 4);
+            b4 = (it - n1 * (B / 4)) * 4;
+        }
+    }
+
+    // The shared profile (prof_rows == 1: one PCHIP row for every channel,
+    // e.g. C3's GaussProfile) is a function of the sample alone, so it is
+    // evaluated once per run instead of once per pair: entry cbx (N1 B / 4) +
+    // it holds samples n .. n + 3 of item it of column block cbx, so each
+    // pass-A workgroup reads one contiguous 4 N1 B-byte block (a wave 1 KB per
+    // item) in place of a phase walk, an LDS gather and a cubic per sample.
+    // The same integer walk and the same fused cubic as the per-pair form:
+    // bitwise its values.
+    __device__ static void prof_cols(const KP &k, float4 *out) {
+        const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (e >= k.N / 4) return;
+        constexpr int IPB = N1 * B / 4;                 // items per column block
+        const int cbx = (int)(e / IPB), it = (int)(e - (int64_t)cbx * IPB);
+        int n1, b4;
+        item_of(it, n1, b4);
+        const PssPipeline &p = k.p;
+        const uint32_t n = (uint32_t)(n1 * (int)k.N2) + (uint32_t)(cbx * B) + (uint32_t)b4;   // N < 2^24
+        uint32_t dlo;
+        uint64_t dhi;
+        phase_delta(p, dlo, dhi);
+        const float4 *prof = reinterpret_cast<const float4 *>(p.prof);
+        PhaseWalk w;
+        w.start(p, n);
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint32_t iv;
+            float u;
+            if (i) w.step(dlo, dhi, p.knot_m);
+            w.get_full(iv, u);
+            const float4 A = prof[iv];
+            v[i] = fmaf(fmaf(fmaf(A.x, u, A.y), u, A.z), u, A.w);
+        }
+        out[e] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+
     // A: generate channels a, b into z = d_a + i d_b; column FFTs; twiddle; spill.
     // FAST (host-selected): search-mode source with Philox chi2(1) draws, no
     // injected draws, no undelayed null -- the same values as source4.
@@ -1581,7 +1638,28 @@ struct PairCols<N1, B, T, RList<F...>, RList<I...>, XRS> {
         const int pra = (p.prof_rows == 1) ? 0 : (int)ca - p.prof_row0, prb = (p.prof_rows == 1) ? 0 : (int)cb - p.prof_row0;
         const Rng g(p.seed, p.call_gen, P_PULSE);
         static_assert(!FAST || kItemsExact, "fast pass A: whole items per thread");
-        if constexpr (FAST) {
+        if constexpr (FAST && SHARED && kPcol) {
+            // the profile from the per-run sample table (prof_cols): loads
+            // issued first, under the Philox draws
+            const float dna = hasa ? p.draw_norm : 0.f, dnb = hasb ? p.draw_norm : 0.f;
+            const float4 *pc = k.pcol + (int64_t)cbx * (N1 * B / 4);
+            float4 P[ITEMS];
+#pragma unroll
+            for (int t = 0; t < ITEMS; ++t) P[t] = pc[tid + t * T];
+#pragma unroll
+            for (int t = 0; t < ITEMS; ++t) {
+                const int it = tid + t * T;
+                int n1, b4;
+                item_of(it, n1, b4);
+                const uint32_t n = (uint32_t)(n1 * (int)N2) + (uint32_t)n20 + (uint32_t)b4;   // N < 2^24
+                const float4 qa = chi2_1x4(g.bits(n >> 2, ca, 0u), dna);
+                const float4 qb = chi2_1x4(g.bits(n >> 2, cb, 0u), dnb);
+                const float pv[4] = {P[t].x, P[t].y, P[t].z, P[t].w};
+                const float va[4] = {qa.x, qa.y, qa.z, qa.w}, vb[4] = {qb.x, qb.y, qb.z, qb.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) lds[LdsC::at(b4 + i, n1)] = make_float2(pv[i] * va[i], pv[i] * vb[i]);
+            }
+        } else if constexpr (FAST) {
             // The pair's two PCHIP rows are staged in LDS (host guarantees
             // nint <= kFastNint), the items are unrolled and branch-free, so
             // the table reads of an item issue together instead of one
@@ -2189,6 +2267,8 @@ template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairA(KP k) { C::template passA<false>(k); }
 template <typename C, int T, bool SHARED>
 __global__ __launch_bounds__(T) void k_pairA_fast(KP k) { C::template passA<true, SHARED>(k); }
+template <typename C>
+__global__ __launch_bounds__(256) void k_prof_cols(KP k, float4 *out) { C::prof_cols(k, out); }
 template <typename C, int T>
 __global__ __launch_bounds__(T) void k_pairC(KP k) { C::passC(k); }
 template <typename C, int T>
@@ -2362,6 +2442,7 @@ struct WsLayout {
     int64_t odd_tw;                    // odd N: exp(+2 pi i j / (N - 1)), j < N - 1 (cf)
     int64_t rf_tw, rf_B, rf_mx;        // float64 null decisions: e^{2 pi i n/N} [N], B [N/2+1] (double2), row max [nchan]
     int64_t rf_part, rf_list, rf_cnt;  // ... partial spectra [kBsParts][N/2+1] (double2), candidate list, its count
+    int64_t pcol;                      // four-step: the profile at every sample (float4 items, k_prof_cols)
 };
 
 static inline WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
@@ -2383,6 +2464,7 @@ static inline WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
         w.mbits = o; o += al256((int64_t)nchan * (N / 8));   // per-channel null bits
         w.rtab = o;  o += al256(npairs * 2 * 64 * 8);          // row-pass pair ramp factors (RFL <= 64)
         w.wlist = o; o += al256((N / 32) * 4);                 // null fix-up: table words with nulls
+        w.pcol = o;  o += al256(N * 4);                        // shared-profile pass A: profile per sample
     } else if (!filt && is_pow2(N) && N >= 64 && N <= 8192) {
         // single-workgroup lengths: W1 [nchan][N] cf and the float64 null
         // refine's buffers (a delayed null: run_single)
@@ -2424,6 +2506,7 @@ static inline WsLayout ws_layout(int32_t nchan, int64_t N, bool filt = false) {
             const int64_t npairs = ((int64_t)nchan + 2) / 2;
             w.yd = 0;
             w.rtab = al256(npairs * N * 8);
+            w.pcol = o; o += al256(N * 4);
         }
     }
     w.row = o;
@@ -2651,8 +2734,19 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     if (launched) {
     } else if constexpr (PC::kItemsExact) {
         if (fast_source(k.p)) {
-            if (k.p.prof_rows == 1) k_pairA_fast<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
-            else k_pairA_fast<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
+            if (k.p.prof_rows == 1) {
+                if constexpr (kPcol) {
+                    float4 *pcol = reinterpret_cast<float4 *>(reinterpret_cast<char *>(k.p.work) +
+                                                              ws_layout(k.p.nchan, k.N).pcol);
+                    const int64_t ne = k.N / 4;
+                    k_prof_cols<PC><<<dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st>>>(k, pcol);
+                    LAUNCHCHK();
+                    k.pcol = pcol;
+                }
+                k_pairA_fast<PC, T, true><<<gc, dim3(T), 0, st>>>(k);
+            } else {
+                k_pairA_fast<PC, T, false><<<gc, dim3(T), 0, st>>>(k);
+            }
             plan_note(k.p.prof_rows == 1 ? " A:fast_shared" : " A:fast");
         } else {
             k_pairA<PC, T><<<gc, dim3(T), 0, st>>>(k);
