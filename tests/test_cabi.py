@@ -52,8 +52,9 @@ def test_workspace_sizes():
     # per-channel mask spill
     table = n * 8 + 6 * n * 8 + 12 * n * 4 + (n // 32) * 8 + (n // 32) * 4 + n * 16 * 4 + 256
     wl = (n // 32) * 4
-    assert L.pss_workspace_bytes(4, n) == 3 * n * 8 + table + 4 * n // 8 + 3 * 1024 + wl + n * 4
-    assert L.pss_workspace_bytes(3, n) == 2 * n * 8 + table + 3 * n // 8 + 2 * 1024 + wl + n * 4
+    pc = n * 4      # (round 6) the shared-profile pass A's per-run sample table
+    assert L.pss_workspace_bytes(4, n) == 3 * n * 8 + table + 4 * n // 8 + 3 * 1024 + wl + pc + n * 4
+    assert L.pss_workspace_bytes(3, n) == 2 * n * 8 + table + 3 * n // 8 + 2 * 1024 + wl + pc + n * 4
     a = lambda b: ((b + 255) // 256) * 256
     # even N <= 2^17 on the fallback paths: + the float64 null decisions'
     # e^{2 pi i n/N} [N] and box spectrum [N/2 + 1] (double2), row maxima [nchan]
