@@ -2657,7 +2657,14 @@ SideStreams *side_streams();
 
 template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typename RF, typename RI,
           int TRF, int BC, int TC>
-static int launch_pair_passes(KP &k, hipStream_t st);
+static int launch_pair_passes(KP &k, hipStream_t st, const float *mask_after_a = nullptr);
+// Channel count up to which the side-stream mask table forks after pass A
+// (beside the row pass) instead of before it (beside pass A): it costs the
+// pass it runs beside ~0.4 ms either way, which at 2048 channels is even
+// (46.84-46.89 vs 46.86-47.06 ms per C3 step) and at 256 channels -- a short
+// pass A it slowed by a quarter -- 0.12 ms per step less after pass A
+// (6.52-6.56 vs 6.64-6.68 ms, profiles/r06/ab_mask/)
+static constexpr int kMaskAfterANchan = 512;
 
 // BC/TC: column-block width and threads of the FAST pass C (the spill layout
 // does not depend on the block width, so pass C may use wider blocks than pass
@@ -2674,6 +2681,7 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
     char *w = reinterpret_cast<char *>(k.p.work);
     const WsLayout L = ws_layout(k.p.nchan, k.N);
     k.Yd = reinterpret_cast<cf *>(w + L.yd);
+    const float *defer_mask = nullptr;
     if (k.p.null_mode == PSS_NULL_DELAYED) {
         // the mask table's position arithmetic is for N = 2^m (validate()
         // sends delayed nulls of other lengths to the direct path)
@@ -2683,14 +2691,20 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
             // pass A (its dozen small launches then cost no time on the main
             // stream); the fix-up waits for it.
             SideStreams *ss = k.p.data_in_fft ? side_streams() : nullptr;
+            if (ss && k.p.nchan <= kMaskAfterANchan) {
+                defer_mask = mask_row;            // built by launch_pair_passes after pass A
+                goto mask_done;
+            }
             hipStream_t ms = st;
             if (ss) {
                 HIPCHK(hipEventRecord(ss->ev[30], st));
                 HIPCHK(hipStreamWaitEvent(ss->s[0], ss->ev[30], 0));
                 ms = ss->s[0];
             }
-            const int rc = build_mask_table<N1, B, T, CF, CI, N2, TR, RF, RI, TRF>(k, ms, mask_row, w, L);
-            if (rc) return rc;
+            {
+                const int rc = build_mask_table<N1, B, T, CF, CI, N2, TR, RF, RI, TRF>(k, ms, mask_row, w, L);
+                if (rc) return rc;
+            }
             if (ss) {
                 HIPCHK(hipEventRecord(ss->ev[31], ms));
                 k.mask_ready = ss->ev[31];
@@ -2700,6 +2714,7 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
                         (long long)k.N);
         }
     }
+mask_done:
     if (!k.p.data_in_fft) {
         // only the null mask was delayed: one elementwise pass with table lookups
         return launch_elementwise(k, st);
@@ -2711,13 +2726,13 @@ static int launch_pair(KP &k, hipStream_t st, const float *mask_row) {
         LAUNCHCHK();
         k.rtab = rt;
     }
-    return launch_pair_passes<N1, B, T, CF, CI, N2, TR, RF, RI, TRF, BC, TC>(k, st);
+    return launch_pair_passes<N1, B, T, CF, CI, N2, TR, RF, RI, TRF, BC, TC>(k, st, defer_mask);
 }
 
 // The passes of one pair range (after the mask table and the ramp table).
 template <int N1, int B, int T, typename CF, typename CI, int N2, int TR, typename RF, typename RI,
           int TRF, int BC, int TC>
-static int launch_pair_passes(KP &k, hipStream_t st) {
+static int launch_pair_passes(KP &k, hipStream_t st, const float *mask_after_a) {
     using PC = PairCols<N1, B, T, CF, CI, xrs_read(B)>;
     using PCC = PairCols<N1, BC, TC, CF, CI, xrs_write(BC)>;
     using PR = PairRows<N2, TR, RF, RI>;
@@ -2758,6 +2773,20 @@ static int launch_pair_passes(KP &k, hipStream_t st) {
     }
     tk_end(st);
     LAUNCHCHK();
+    if constexpr ((N1 & (N1 - 1)) == 0 && N2 <= 8192) {
+        if (mask_after_a) {
+            // (kMaskAfterANchan) the mask table on the side stream from here
+            SideStreams *ss = side_streams();
+            char *w = reinterpret_cast<char *>(k.p.work);
+            const WsLayout L = ws_layout(k.p.nchan, k.N);
+            HIPCHK(hipEventRecord(ss->ev[30], st));
+            HIPCHK(hipStreamWaitEvent(ss->s[0], ss->ev[30], 0));
+            const int rc = build_mask_table<N1, B, T, CF, CI, N2, TR, RF, RI, TRF>(k, ss->s[0], mask_after_a, w, L);
+            if (rc) return rc;
+            HIPCHK(hipEventRecord(ss->ev[31], ss->s[0]));
+            k.mask_ready = ss->ev[31];
+        }
+    }
     tk_begin(TK_ROW, st);
     if constexpr (N2 > 8192) {
         // 16384-point rows (C5's 1024 x 16384 split): one row at a time

@@ -1,6 +1,7 @@
 // pss_fourstep.hip -- the power-of-two four-step: the dispatch, C3's 2^22 (other
 // lengths: pss_fourstep_b.hip), the delayed-null mask-table kernels and fix-up.
 #include "pss_engine.hpp"
+#include <algorithm>
 
 using namespace pss;
 
@@ -190,10 +191,33 @@ __global__ __launch_bounds__(256) void k_mask_table(const float *nodes, int64_t 
         base[(p >> 5) + 1] = b0 + (uint32_t)__popc((uint32_t)ab);
     }
     if (amb) {
-        // root record (root_hit): where the fp32 Clenshaw value crosses 1,
-        // on a certified scan grid (see root_hit)
-        const float4 q[3] = {make_float4(c[0], c[1], c[2], c[3]), make_float4(c[4], c[5], c[6], c[7]),
-                             make_float4(c[8], c[9], c[10], c[11])};
+        // the position's coefficients, compacted; k_mask_roots turns them
+        // into its root record (the scan's cost is per f-dependent position:
+        // run here, every wave holding one such position would run it for
+        // all 64 lanes)
+        const uint32_t idx = b0 + (uint32_t)__popcll(ab & ((1ull << lane) - 1ull));
+        float4 *dst = reinterpret_cast<float4 *>(coef + (int64_t)idx * KREC);
+        dst[1] = make_float4(c[0], c[1], c[2], c[3]);
+        dst[2] = make_float4(c[4], c[5], c[6], c[7]);
+        dst[3] = make_float4(c[8], c[9], c[10], c[11]);
+    }
+}
+
+// Root records of the f-dependent positions (compacted by k_mask_table, which
+// left each one's Chebyshev coefficients in its record): where the fp32
+// Clenshaw value crosses 1, on a certified scan grid (see root_hit).  One
+// position per lane, grid-stride over the device-side count: the same
+// arithmetic as the scan had inside k_mask_table, bitwise the same records.
+__global__ __launch_bounds__(256) void k_mask_roots(float *coef, const uint32_t *counter) {
+    const uint32_t na = *counter;
+    for (uint32_t idx = blockIdx.x * 256u + threadIdx.x; idx < na; idx += gridDim.x * 256u) {
+        float4 *dst = reinterpret_cast<float4 *>(coef + (int64_t)idx * KREC);
+        const float4 q[3] = {dst[1], dst[2], dst[3]};
+        const float c[KCH] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w,
+                              q[2].x, q[2].y, q[2].z, q[2].w};
+        float S = 0.f;
+#pragma unroll
+        for (int n = 1; n < KCH; ++n) S += fabsf(c[n]);
         float D2 = 0.f;                              // max |g''| on [-1, 1] (Markov)
 #pragma unroll
         for (int n = 2; n < KCH; ++n) {
@@ -235,8 +259,6 @@ __global__ __launch_bounds__(256) void k_mask_table(const float *nodes, int64_t 
             gprev = g;
             tprev = tg;
         }
-        const uint32_t idx = b0 + (uint32_t)__popcll(ab & ((1ull << lane) - 1ull));
-        float4 *dst = reinterpret_cast<float4 *>(coef + (int64_t)idx * KREC);
         if (cert && cnt <= 10) {
             dst[0] = make_float4((float)cnt, s0 ? 1.0f : 0.0f, rt[0], rt[1]);
             dst[1] = make_float4(rt[2], rt[3], rt[4], rt[5]);
@@ -258,6 +280,9 @@ int launch_node_params(uint64_t *ramp, float *nyq, int L, hipStream_t st) {
 int launch_mask_table(const float *nodes, int64_t N, uint2 *bits, uint32_t *base, float *coef, uint32_t *counter,
                       hipStream_t st) {
     k_mask_table<<<dim3((unsigned)(N / 256)), dim3(256), 0, st>>>(nodes, N, bits, base, coef, counter);
+    LAUNCHCHK();
+    const unsigned gr = (unsigned)std::min<int64_t>(N / 256, 1024);
+    k_mask_roots<<<dim3(gr), dim3(256), 0, st>>>(coef, counter);
     LAUNCHCHK();
     return PSS_OK;
 }
