@@ -2661,10 +2661,14 @@ static int launch_pair_passes(KP &k, hipStream_t st, const float *mask_after_a =
 // Channel count up to which the side-stream mask table forks after pass A
 // (beside the row pass) instead of before it (beside pass A): it costs the
 // pass it runs beside ~0.4 ms either way, which at 2048 channels is even
-// (46.84-46.89 vs 46.86-47.06 ms per C3 step) and at 256 channels -- a short
-// pass A it slowed by a quarter -- 0.12 ms per step less after pass A
-// (6.52-6.56 vs 6.64-6.68 ms, profiles/r06/ab_mask/)
-static constexpr int kMaskAfterANchan = 512;
+// (46.84-46.89 vs 46.86-47.06 ms per C3 step), at 1024 channels slightly
+// better after pass A (kernels 23.05-23.12 vs 23.17-23.20 ms) and at 256
+// channels -- a short pass A it slowed by a quarter -- 0.12 ms per step less
+// after pass A (6.52-6.56 vs 6.64-6.68 ms, profiles/r06/ab_mask/)
+#ifndef PSS_MASK_AFTER_A_NCHAN
+#define PSS_MASK_AFTER_A_NCHAN 1024
+#endif
+static constexpr int kMaskAfterANchan = PSS_MASK_AFTER_A_NCHAN;
 
 // BC/TC: column-block width and threads of the FAST pass C (the spill layout
 // does not depend on the block width, so pass C may use wider blocks than pass
