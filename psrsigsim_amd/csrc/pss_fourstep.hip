@@ -235,20 +235,22 @@ __global__ __launch_bounds__(256) void k_mask_roots(float *coef, const uint32_t 
         const bool s0 = prev;
         bool cert = true;
         int cnt = 0;
-        float tprev = -1.0f;
+        // the scan records the cells [t_{jg-1}, t_jg] where the decision flips
+        // (grid points -1 + jg H are exact); the bisections run afterwards,
+        // flip i of every lane together, so a wave pays 24 evaluations per
+        // flip of its busiest lane rather than per flip of every lane (the
+        // same brackets and evaluations: bitwise the same roots)
+        int jf[10];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) jf[i] = 0;
         for (int jg = 1; jg <= NG; ++jg) {
             const float tg = -1.0f + (float)jg * H;
             const float g = cheb_eval_r(q, tg) - 1.0f;
             const bool cur = g > 0.0f;
             if (cur != prev) {
                 cert = cert && (fabsf(g - gprev) - 2.0f * err > D2 * H * H);   // one flip only
-                float lo = tprev, hi = tg;            // decision prev at lo, cur at hi
-                for (int it = 0; it < 24; ++it) {
-                    const float mid = 0.5f * (lo + hi);
-                    if ((cheb_eval_r(q, mid) > 1.0f) == prev) lo = mid; else hi = mid;
-                }
 #pragma unroll
-                for (int i = 0; i < 10; ++i) if (i == cnt) rt[i] = lo;
+                for (int i = 0; i < 10; ++i) if (i == cnt) jf[i] = jg;
                 ++cnt;
             } else {
                 // no flip: g stays within D2 H^2 / 8 of the chord between the
@@ -257,7 +259,20 @@ __global__ __launch_bounds__(256) void k_mask_roots(float *coef, const uint32_t 
             }
             prev = cur;
             gprev = g;
-            tprev = tg;
+        }
+        const int nb = cnt < 10 ? cnt : 10;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            if (i < nb) {
+                // the decisions alternate from s0: before flip i it is s0 for even i
+                const bool pv = (i & 1) ? !s0 : s0;
+                float lo = -1.0f + (float)(jf[i] - 1) * H, hi = -1.0f + (float)jf[i] * H;
+                for (int it = 0; it < 24; ++it) {
+                    const float mid = 0.5f * (lo + hi);
+                    if ((cheb_eval_r(q, mid) > 1.0f) == pv) lo = mid; else hi = mid;
+                }
+                rt[i] = lo;
+            }
         }
         if (cert && cnt <= 10) {
             dst[0] = make_float4((float)cnt, s0 ? 1.0f : 0.0f, rt[0], rt[1]);
